@@ -1,0 +1,141 @@
+"""TEST INFRASTRUCTURE ONLY -- the CPU parity oracle.
+
+``oracle/wgrt_oracle.c`` restates the reference kernel
+``process_rays_kernel_pro_fullColor`` (GPU_ray_tracing_functions.py:833-1246)
+in plain float64 C; this module loads it with ctypes.  Only ``tests/``,
+``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
+it -- as the checker / the timed CPU baseline, never as a product path.
+
+Parity: pinned by the golden fixtures under ``tests/golden`` (generated from the
+reference's own kernel code, see ``tests/golden/gen_golden.py``).
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(HERE, "build", "libwgrt_oracle.so")
+
+_f64p = ctypes.POINTER(ctypes.c_double)
+_f32p = ctypes.POINTER(ctypes.c_float)
+_i64p = ctypes.POINTER(ctypes.c_int64)
+_u32p = ctypes.POINTER(ctypes.c_uint32)
+
+
+class _Scene(ctypes.Structure):
+    _fields_ = [
+        ("ic", _f64p), ("n_ic", ctypes.c_int64),
+        ("fc", _f64p), ("fc_offset", _i64p), ("n_fc_slices", ctypes.c_int64),
+        ("oc", _f64p), ("oc_offset", _i64p), ("n_oc_slices", ctypes.c_int64),
+        ("eff1", _f64p), ("n_eff1", ctypes.c_int64),
+        ("eff2", _f64p), ("n_eff2", ctypes.c_int64),
+        ("eff_reg_fov", _f64p), ("eff_reg_fov_range", _f64p),
+        ("lut_tir", _f64p), ("lut_gap", _f64p),
+        ("ic1", _f64p), ("ic2", _f64p), ("ic3", _f64p),
+        ("fc1", _f64p), ("fc2", _f64p), ("oc1", _f64p), ("oc2", _f64p),
+        ("num_lmd", ctypes.c_int32), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
+        ("ch5", ctypes.c_int32), ("ch3", ctypes.c_int32),
+        ("n_g", ctypes.c_double),
+    ]
+
+
+class _Rays(ctypes.Structure):
+    _fields_ = [(k, _f32p) for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")]
+
+
+_lib = None
+
+
+def build(quiet: bool = True) -> str:
+    """Compile the oracle with the committed Makefile (gcc + OpenMP)."""
+    out = subprocess.run(["make", "-C", HERE], capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("oracle build failed:\n" + out.stdout + out.stderr)
+    return LIB_PATH
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            build()
+        L = ctypes.CDLL(LIB_PATH)
+        L.wgrt_oracle_trace.restype = ctypes.c_int64
+        L.wgrt_oracle_trace.argtypes = [ctypes.POINTER(_Scene), ctypes.POINTER(_Rays), ctypes.c_int64,
+                                        ctypes.c_int64, _u32p, _f32p, _u32p, ctypes.POINTER(ctypes.c_uint8),
+                                        ctypes.c_int]
+        L.wgrt_oracle_hypot.restype = ctypes.c_double
+        L.wgrt_oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
+        L.wgrt_oracle_wrap.restype = ctypes.c_double
+        L.wgrt_oracle_wrap.argtypes = [ctypes.c_double]
+        L.wgrt_oracle_inside.restype = ctypes.c_int
+        L.wgrt_oracle_inside.argtypes = [ctypes.c_double, ctypes.c_double, _f64p, ctypes.c_int64]
+        L.wgrt_oracle_xorshift.restype = ctypes.c_uint32
+        L.wgrt_oracle_xorshift.argtypes = [ctypes.c_uint32, ctypes.c_int64, _f64p]
+        _lib = L
+    return _lib
+
+
+def _p(a, t):
+    return a.ctypes.data_as(t)
+
+
+class OracleScene:
+    """Geometry + LUT arrays in the reference's layout, held alive for the C side."""
+
+    def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
+                 eff_reg_FOV_range, luts: dict, lut_TIR, lut_gap):
+        c = lambda a, dt=np.float64: np.ascontiguousarray(a, dtype=dt)
+        self._keep = dict(
+            IC=c(IC), FC=c(FC), FC_offset=c(FC_offset, np.int64), OC=c(OC), OC_offset=c(OC_offset, np.int64),
+            eff1=c(eff_reg1), eff2=c(eff_reg2), fov=c(eff_reg_FOV), rng=c(eff_reg_FOV_range),
+            tir=c(lut_TIR), gap=c(lut_gap),
+            **{k: c(luts[k], np.complex128) for k in ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1",
+                                                       "lut_fc2", "lut_oc1", "lut_oc2")})
+        k = self._keep
+        L, NX, NY = k["tir"].shape[:3]
+        self.num_lmd, self.nx, self.ny = L, NX, NY
+        self._s = _Scene(
+            _p(k["IC"], _f64p), k["IC"].shape[0],
+            _p(k["FC"], _f64p), _p(k["FC_offset"], _i64p), k["FC_offset"].shape[0] - 1,
+            _p(k["OC"], _f64p), _p(k["OC_offset"], _i64p), k["OC_offset"].shape[0] - 1,
+            _p(k["eff1"], _f64p), k["eff1"].shape[0], _p(k["eff2"], _f64p), k["eff2"].shape[0],
+            _p(k["fov"], _f64p), _p(k["rng"], _f64p), _p(k["tir"], _f64p), _p(k["gap"], _f64p),
+            *[k[n].ctypes.data_as(_f64p) for n in ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1",
+                                                   "lut_fc2", "lut_oc1", "lut_oc2")],
+            L, NX, NY, k["lut_ic1"].shape[-1], k["lut_fc1"].shape[-1], float(n_g))
+
+    @classmethod
+    def from_geometry(cls, geom, luts):
+        return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
+                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts, geom.lut_TIR,
+                   geom.lut_gap)
+
+    def eb_shape(self):
+        return (self.num_lmd, self.ny, self.nx, 80, 120)
+
+    def trace(self, rays: dict, rng: np.ndarray, eb: np.ndarray, gid_offset: int = 0,
+              threads: int = 0, per_ray_bounces: bool = False, fate: bool = False):
+        """One launch over the shard ``rays`` (mutates ``rng`` and ``eb``).
+
+        Returns ``(total_bounces, per_ray_counts_or_None)``, plus the per-ray fate codes
+        when ``fate`` is set."""
+        cols = {k: np.ascontiguousarray(rays[src], dtype=np.float32) for k, src in
+                (("x", "x"), ("y", "y"), ("m", "m"), ("n", "n"), ("lmd", "lmd_num"), ("te", "te"),
+                 ("tm", "tm"), ("dph", "delta_phase"))}
+        N = cols["x"].shape[0]
+        assert rng.dtype == np.uint32 and rng.flags.c_contiguous and rng.shape == (N,)
+        assert eb.dtype == np.float32 and eb.flags.c_contiguous and eb.shape == self.eb_shape()
+        r = _Rays(*[_p(cols[k], _f32p) for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")])
+        counts = np.zeros(N, dtype=np.uint32) if per_ray_bounces else None
+        fates = np.zeros(N, dtype=np.uint8) if fate else None
+        tot = lib().wgrt_oracle_trace(ctypes.byref(self._s), ctypes.byref(r), N, int(gid_offset),
+                                      _p(rng, _u32p), _p(eb, _f32p),
+                                      _p(counts, _u32p) if counts is not None else None,
+                                      fates.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if fate else None,
+                                      int(threads))
+        return (int(tot), counts, fates) if fate else (int(tot), counts)

@@ -1,0 +1,55 @@
+"""Pin the CPU oracle (oracle/wgrt_oracle.c) to the reference's own kernel outputs.
+
+The fixtures were produced by running GPU_ray_tracing_functions.py:833-1246
+unmodified (tests/golden/gen_golden.py).  Bar: bit-exact rng_states,
+matrix_EB and per-ray bounce counts after 1 and after 4 launches.
+"""
+import numpy as np
+import pytest
+
+from oracle import OracleScene
+from tests._fixtures import CASES, GoldenCase
+
+
+@pytest.fixture(scope="module", params=CASES)
+def case(request):
+    return GoldenCase(request.param)
+
+
+def test_inputs_regenerate_bit_identically(case):
+    assert case.digest_ok(), "geometry / synthetic-LUT generator drifted from the fixture"
+
+
+@pytest.mark.parametrize("threads", [1, 4])
+def test_oracle_matches_reference(case, threads):
+    sc = OracleScene.from_geometry(case.geom, case.luts)
+    rng = case.fresh_rng()
+    eb = np.zeros(case.eb_shape(), np.float32)
+    num_iter = int(case.f["num_iter"])
+    for it in range(num_iter):
+        tot, per_ray = sc.trace(case.rays, rng, eb, threads=threads, per_ray_bounces=True)
+        np.testing.assert_array_equal(per_ray, case.f["bounces"][it])
+        assert tot == int(case.f["bounces"][it].sum())
+        if it == 0:
+            np.testing.assert_array_equal(rng, case.f["rng_after1"])
+            np.testing.assert_array_equal(eb, case.eb_expected(1))
+    np.testing.assert_array_equal(rng, case.f["rng_after4"])
+    np.testing.assert_array_equal(eb, case.eb_expected(4))
+
+
+def test_oracle_sharding_invariance(case):
+    """Tracing R-aligned gid ranges separately (with gid_offset) equals one pass."""
+    sc = OracleScene.from_geometry(case.geom, case.luts)
+    rng_full = case.fresh_rng()
+    eb_full = np.zeros(case.eb_shape(), np.float32)
+    sc.trace(case.rays, rng_full, eb_full)
+    rng_sh = case.fresh_rng()
+    eb_sh = np.zeros(case.eb_shape(), np.float32)
+    cuts = [0, case.R, 3 * case.R, case.N]
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        part = {k: v[a:b] for k, v in case.rays.items()}
+        r = np.ascontiguousarray(rng_sh[a:b])
+        sc.trace(part, r, eb_sh, gid_offset=a)
+        rng_sh[a:b] = r
+    np.testing.assert_array_equal(rng_sh, rng_full)
+    np.testing.assert_array_equal(eb_sh, eb_full)
