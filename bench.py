@@ -1,0 +1,202 @@
+#!/usr/bin/env python3
+"""Benchmark: ray-bounces/s of the full-colour waveguide bounce kernel on MI355X.
+
+BASELINE.json metric: "ray-bounces/sec, full-color 21x21 FoV, num_rays_per_FoV=1024;
+1/2/4/8 GPU".  A ray-bounce = 1 in-coupling event + 1 per executed iteration of the
+reference's bounce loop (GRTF:860-905); counted on the device by the kernel itself.
+
+One step = one launch of the bounce kernel over the whole per-rank batch (one of the
+reference's ``num_iter`` launches, gpu_ray_tracing_pro_fullColor.py:169-177), plus, at
+N > 1, the RCCL reduce of the eyebox grid to rank 0.  Inputs (ray SoA, RNG, scene) are
+resident in HBM before timing starts.
+
+Multi-GPU (weak scaling): the job at N GPUs traces num_rays_per_FoV = 1024 * N rays per
+FoV x wavelength block and shards the blocks (contiguous global-ray ranges) over the
+ranks, so every rank traces 21 x 21 x 3 x 1024 rays per step, with its global ray ids
+(RNG seeds are global, results independent of N).  Launch:
+    python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import math
+import os
+import sys
+import time
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, REPO)
+
+ALGO_BYTES_PER_BOUNCE = 72      # read + write of the minimal 36-B ray record
+HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
+
+
+def parse():
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--nx", type=int, default=21)
+    ap.add_argument("--ny", type=int, default=21)
+    ap.add_argument("--rays-per-fov", type=int, default=1024, help="per GPU (weak scaling)")
+    ap.add_argument("--lambdas", default="0,1,2")
+    ap.add_argument("--lut-profile", default="default")
+    ap.add_argument("--lut-seed", type=int, default=0)
+    ap.add_argument("--variant", type=int, default=0, help="0 auto, 1 grid, 2 persistent")
+    ap.add_argument("--workgroups", type=int, default=0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
+                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
+    return ap.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, rays_to_device, trace_fullcolor
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import (build_rays, generate_points_in_polygon,
+                                                                         rng_seeds)
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != a.gpus:
+        raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    dev = torch.device("cuda", local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=dev)
+
+    lambdas = [int(v) for v in a.lambdas.split(",")]
+    nx, ny = a.nx, a.ny
+    R = a.rays_per_fov * world                 # global rays per FoV x lambda block
+    nblk = nx * ny * len(lambdas)
+    lo, hi = rank * nblk // world, (rank + 1) * nblk // world
+    geom = design_geometry(nx, ny)
+    luts = synthetic_luts(geom, seed=a.lut_seed, profile=a.lut_profile)
+    points = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
+    host_rays = build_rays(points, nx, ny, lambdas, R, blocks=(lo, hi))
+    n_local = host_rays["x"].shape[0]
+    gid0 = lo * R
+    scene = Scene.from_geometry(geom, luts, device=local)
+    rays = rays_to_device(host_rays, dev)
+    seeds = rng_seeds(n_local, gid0)
+    rng = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+
+    def step(timed_events=None):
+        if timed_events is not None:
+            timed_events[0].record()
+        trace_fullcolor(scene, rays, rng, eb, gid_offset=gid0, stats=stats, variant=a.variant,
+                        workgroups=a.workgroups)
+        if timed_events is not None:
+            timed_events[1].record()
+        if world > 1:
+            dist.reduce(eb, dst=0, op=dist.ReduceOp.SUM)
+
+    for _ in range(a.warmup):
+        step()
+    torch.cuda.synchronize()
+    stats.zero_()
+    events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in range(a.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for k in range(a.steps):
+        step(events[k])
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    kern_ms = [s.elapsed_time(e) for s, e in events]
+    bounces_local = int(stats[0].item())
+    t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+    b = torch.tensor([bounces_local], dtype=torch.int64, device=dev)
+    if world > 1:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM)
+    elapsed = float(t.item())
+    bounces_total = int(b.item())
+    value = bounces_total / elapsed
+
+    if rank == 0:
+        kavg_s = float(np.mean(kern_ms)) / 1e3
+        bounces_per_launch_local = bounces_local / a.steps
+        achieved = bounces_per_launch_local * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
+        cfg_key = f"{nx}x{ny}x{len(lambdas)}xR{a.rays_per_fov}:{a.lut_profile}:{a.lut_seed}:v{a.variant}"
+        traffic = None
+        try:
+            with open(a.traffic_json) as f:
+                traffic = json.load(f).get(cfg_key, {}).get("hbm_bytes_per_launch")
+        except (OSError, ValueError):
+            pass
+        roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+                    "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
+                    "kernel": "trace_grid_kernel" if a.variant in (0, 1) else "trace_persistent_kernel",
+                    "kernel_avg_ms": round(kavg_s * 1e3, 4),
+                    "algo_bytes_per_bounce": ALGO_BYTES_PER_BOUNCE,
+                    "bounces_per_launch": int(round(bounces_per_launch_local))}
+        cpu = None
+        if world == 1 and not a.no_cpu_baseline:
+            cpu = cpu_baseline(geom, luts, points, nx, ny, lambdas, R, a.cpu_seconds)
+        line = {
+            "metric": "ray-bounces/sec, full-color 21x21 FoV, num_rays_per_FoV=1024",
+            "value": round(value, 1), "unit": "ray-bounces/s", "n_gpus": world, "steps": a.steps,
+            "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+            "config": {"workload": f"full-colour {nx}x{ny} FoV x {len(lambdas)} lambda, "
+                                   f"num_rays_per_FoV={a.rays_per_fov} per GPU (BASELINE config 3)",
+                       "nx": nx, "ny": ny, "lambdas": lambdas, "rays_per_fov_per_gpu": a.rays_per_fov,
+                       "rays_per_gpu": n_local, "lut": f"synthetic seed {a.lut_seed} profile {a.lut_profile}",
+                       "geometry": "couplers_coor_full_color restatement",
+                       "parallelism": f"fov-lambda block shards x{world}" + (" + RCCL reduce(EB)" if world > 1 else ""),
+                       "kernel_variant": a.variant},
+            "roofline": roofline,
+            "cpu_baseline": cpu,
+        }
+        print(json.dumps(line), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
+def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):
+    """Time the CPU oracle (oracle/wgrt_oracle.c, float64, OpenMP) on the leading
+    FoV x lambda blocks of the same workload (fresh RNG), sized to ~target_s seconds."""
+    from oracle import OracleScene
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    threads = min(threads, os.cpu_count() or threads)
+    sc = OracleScene.from_geometry(geom, luts)
+    nblk = nx * ny * len(lambdas)
+
+    def run(nb):
+        rays = build_rays(points, nx, ny, lambdas, R, blocks=(0, nb))
+        rng = rng_seeds(rays["x"].shape[0])
+        eb = np.zeros(sc.eb_shape(), np.float32)
+        t = time.perf_counter()
+        tot, _ = sc.trace(rays, rng, eb, threads=threads)
+        return tot, time.perf_counter() - t
+
+    probe = max(1, min(nblk, 8))
+    tot, dt = run(probe)
+    rate_per_blk = dt / probe
+    nb = int(max(1, min(nblk, target_s / max(rate_per_blk, 1e-9))))
+    tot, dt = run(nb)
+    return {"value": round(tot / dt, 1), "unit": "ray-bounces/s", "cores": threads, "kind": "port",
+            "sample": f"first {nb} of {nblk} FoV x lambda blocks x {R} rays, one launch, fresh RNG "
+                      f"({tot} bounces in {dt:.2f} s); oracle/wgrt_oracle.c float64 OpenMP"}
+
+
+if __name__ == "__main__":
+    main()

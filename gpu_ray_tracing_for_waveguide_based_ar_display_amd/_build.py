@@ -1,0 +1,56 @@
+"""Build the in-tree HIP library ``libwgrt.so`` for gfx950 (hipcc, no JIT cache).
+
+Called by ``__graft_entry__.build()``; safe to call repeatedly (rebuilds only when a
+source is newer than the library).
+"""
+from __future__ import annotations
+
+import os
+import shutil
+import subprocess
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+CSRC = os.path.join(PKG, "csrc")
+REPO = os.path.dirname(PKG)
+LIB = os.path.join(PKG, "libwgrt.so")
+SOURCES = ["wgrt_trace.hip", "wgrt_scene_build.cpp"]
+HEADERS = ["wgrt_common.h", "wgrt_scene_build.h"]
+ARCH = os.environ.get("WGRT_OFFLOAD_ARCH", "gfx950")
+
+# -ffp-contract=off: the reference never fuses a*b+c (Python float semantics); keeping
+# every product / sum separately rounded is what makes the results bit-reproducible.
+FLAGS = ["-O3", "-std=c++17", "-fPIC", "-shared", "-ffp-contract=off", "-fno-fast-math",
+         "-Wall", "-Wno-unused-function", f"--offload-arch={ARCH}"]
+
+
+def _hipcc() -> str:
+    for cand in (os.environ.get("HIPCC"), "/opt/rocm/bin/hipcc", shutil.which("hipcc")):
+        if cand and os.path.exists(cand):
+            return cand
+    raise RuntimeError("hipcc not found (set HIPCC or install ROCm)")
+
+
+def _stale() -> bool:
+    if not os.path.exists(LIB):
+        return True
+    t = os.path.getmtime(LIB)
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", "wgrt.h")]
+    return any(os.path.getmtime(d) > t for d in deps)
+
+
+def build(force: bool = False, verbose: bool = False) -> str:
+    if not force and not _stale():
+        return LIB
+    cmd = [_hipcc(), *FLAGS, "-I", os.path.join(REPO, "include"), "-o", LIB + ".tmp"] + \
+          [os.path.join(CSRC, f) for f in SOURCES]
+    if verbose:
+        print(" ".join(cmd))
+    out = subprocess.run(cmd, capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("hipcc failed:\n" + out.stdout + out.stderr)
+    os.replace(LIB + ".tmp", LIB)
+    return LIB
+
+
+if __name__ == "__main__":
+    print(build(force=True, verbose=True))

@@ -1,0 +1,209 @@
+"""ctypes binding of the in-tree HIP library ``libwgrt.so`` (C ABI: ``include/wgrt.h``).
+
+This is the reference-side binding a Python caller uses; there is no CPU
+fallback: if the library is missing or cannot be loaded, every entry point
+raises ``WgrtError``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+PKG = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(PKG, "libwgrt.so")
+
+ABI_VERSION = 1
+EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
+            "wgrt_trace_fullcolor_ex", "wgrt_scene_classify", "wgrt_selftest_math", "wgrt_status_string",
+            "wgrt_last_error", "wgrt_abi_version")
+
+
+class WgrtError(RuntimeError):
+    pass
+
+
+_d = ctypes.POINTER(ctypes.c_double)
+_i64 = ctypes.POINTER(ctypes.c_int64)
+_f = ctypes.POINTER(ctypes.c_float)
+_vp = ctypes.c_void_p
+
+
+class SceneDesc(ctypes.Structure):
+    _fields_ = [
+        ("IC", _d), ("n_ic", ctypes.c_int64),
+        ("FC", _d), ("FC_offset", _i64), ("n_fc_slices", ctypes.c_int64),
+        ("OC", _d), ("OC_offset", _i64), ("n_oc_slices", ctypes.c_int64),
+        ("n_g", ctypes.c_double),
+        ("eff_reg1", _d), ("n_eff_reg1", ctypes.c_int64),
+        ("eff_reg2", _d), ("n_eff_reg2", ctypes.c_int64),
+        ("eff_reg_FOV", _d), ("eff_reg_FOV_range", _d),
+        ("lut_ic1", _d), ("lut_ic2", _d), ("lut_ic3", _d),
+        ("lut_fc1", _d), ("lut_fc2", _d), ("lut_oc1", _d), ("lut_oc2", _d),
+        ("ch5", ctypes.c_int32), ("ch3", ctypes.c_int32),
+        ("lut_TIR", _d), ("lut_gap", _d),
+        ("num_lmd", ctypes.c_int32), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
+    ]
+
+
+class Rays(ctypes.Structure):
+    _fields_ = [(k, _vp) for k in ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te",
+                                   "tm", "delta_phase")]
+
+
+class TraceStats(ctypes.Structure):
+    _fields_ = [("bounces", ctypes.c_uint64), ("bad_rays", ctypes.c_uint64),
+                ("eyebox_hits", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+
+
+class SceneInfo(ctypes.Structure):
+    _fields_ = [("tile_bytes", ctypes.c_int64), ("tiles", ctypes.c_int64),
+                ("grid_cells_x", ctypes.c_int64), ("grid_cells_y", ctypes.c_int64),
+                ("grid_cell_mm", ctypes.c_double), ("grid_edge_cells", ctypes.c_int64),
+                ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32)]
+
+
+_lib = None
+
+
+def load(path: str = LIB_PATH):
+    """Load libwgrt.so (never builds implicitly: build with ``__graft_entry__.build()``)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(path):
+        raise WgrtError(f"{path} not found: the HIP library is not built "
+                        "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    try:
+        L = ctypes.CDLL(path)
+    except OSError as e:
+        raise WgrtError(f"cannot load {path}: {e}") from e
+    st = ctypes.c_int
+    L.wgrt_scene_create.restype = st
+    L.wgrt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_int, ctypes.POINTER(_vp)]
+    L.wgrt_scene_destroy.restype = st
+    L.wgrt_scene_destroy.argtypes = [_vp]
+    L.wgrt_scene_get_info.restype = st
+    L.wgrt_scene_get_info.argtypes = [_vp, ctypes.POINTER(SceneInfo)]
+    L.wgrt_trace_fullcolor.restype = st
+    L.wgrt_trace_fullcolor.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, _vp, _vp,
+                                       _vp, _vp, _vp]
+    L.wgrt_trace_fullcolor_ex.restype = st
+    L.wgrt_trace_fullcolor_ex.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, _vp,
+                                          _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]
+    L.wgrt_scene_classify.restype = st
+    L.wgrt_scene_classify.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
+    L.wgrt_selftest_math.restype = st
+    L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
+    L.wgrt_status_string.restype = ctypes.c_char_p
+    L.wgrt_status_string.argtypes = [ctypes.c_int]
+    L.wgrt_last_error.restype = ctypes.c_char_p
+    L.wgrt_last_error.argtypes = []
+    L.wgrt_abi_version.restype = ctypes.c_int
+    if L.wgrt_abi_version() != ABI_VERSION:
+        raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} != expected {ABI_VERSION}")
+    _lib = L
+    return L
+
+
+def check(status: int, what: str):
+    if status != 0:
+        L = load()
+        raise WgrtError(f"{what}: {L.wgrt_status_string(status).decode()} -- {L.wgrt_last_error().decode()}")
+
+
+def _ptr(a: np.ndarray, t=_d):
+    return a.ctypes.data_as(t)
+
+
+class Scene:
+    """Device-resident geometry + packed LUT tiles (``wgrt_scene_create``).
+
+    Arguments are the reference's scene arrays (couplers_coor.py:740-750 and the
+    seven LUTs of gpu_ray_tracing_pro_fullColor.py:28-34), as host numpy arrays.
+    """
+
+    def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
+                 eff_reg_FOV_range, lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2,
+                 lut_TIR, lut_gap, device: int = 0):
+        L = load()
+        f64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.float64)
+        c128 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.complex128)
+        i64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.int64)
+        k = dict(IC=f64(IC), FC=f64(FC), FC_offset=i64(FC_offset), OC=f64(OC), OC_offset=i64(OC_offset),
+                 eff1=f64(eff_reg1), eff2=f64(eff_reg2), fov=f64(eff_reg_FOV), fovr=f64(eff_reg_FOV_range),
+                 ic1=c128(lut_ic1), ic2=c128(lut_ic2), ic3=c128(lut_ic3), fc1=c128(lut_fc1),
+                 fc2=c128(lut_fc2), oc1=c128(lut_oc1), oc2=c128(lut_oc2), tir=f64(lut_TIR), gap=f64(lut_gap))
+        for name in ("IC", "FC", "OC", "eff1", "eff2"):
+            a = k[name]
+            if a.ndim != 2 or a.shape[1] != 2:
+                raise ValueError(f"{name} must have shape (V, 2), got {a.shape}")
+        if k["tir"].ndim != 4 or k["tir"].shape[-1] != 4:
+            raise ValueError(f"lut_TIR must have shape (L, NX, NY, 4), got {k['tir'].shape}")
+        nl, nx, ny = k["tir"].shape[:3]
+        nfc, noc = k["FC_offset"].shape[0] - 1, k["OC_offset"].shape[0] - 1
+        want = {"gap": (nl, nx, ny, 8), "fov": (nx, ny, 4, 2), "fovr": (nx, ny, 4)}
+        for name, shp in want.items():
+            if k[name].shape != shp:
+                raise ValueError(f"{name}: shape {k[name].shape} != {shp}")
+        for name in ("ic1", "ic2", "ic3"):
+            if k[name].shape[:3] != (nl, nx, ny):
+                raise ValueError(f"lut_{name}: shape {k[name].shape} does not match grid {(nl, nx, ny)}")
+        for name, ns in (("fc1", nfc), ("fc2", nfc), ("oc1", noc), ("oc2", noc)):
+            if k[name].shape[:4] != (ns, nl, nx, ny):
+                raise ValueError(f"lut_{name}: shape {k[name].shape} does not match {(ns, nl, nx, ny)}")
+        if k["FC_offset"][-1] > k["FC"].shape[0] or k["OC_offset"][-1] > k["OC"].shape[0]:
+            raise ValueError("FC_offset / OC_offset point past the vertex arrays")
+        ch5 = k["ic1"].shape[-1]
+        if not (k["ic2"].shape[-1] == k["ic3"].shape[-1] == k["oc1"].shape[-1] == k["oc2"].shape[-1] == ch5):
+            raise ValueError("ic*/oc* LUTs must share one channel count")
+        ch3 = k["fc1"].shape[-1]
+        if k["fc2"].shape[-1] != ch3:
+            raise ValueError("fc1/fc2 LUTs must share one channel count")
+        desc = SceneDesc(
+            _ptr(k["IC"]), k["IC"].shape[0], _ptr(k["FC"]), _ptr(k["FC_offset"], _i64), nfc,
+            _ptr(k["OC"]), _ptr(k["OC_offset"], _i64), noc, float(n_g),
+            _ptr(k["eff1"]), k["eff1"].shape[0], _ptr(k["eff2"]), k["eff2"].shape[0],
+            _ptr(k["fov"]), _ptr(k["fovr"]),
+            _ptr(k["ic1"]), _ptr(k["ic2"]), _ptr(k["ic3"]), _ptr(k["fc1"]), _ptr(k["fc2"]),
+            _ptr(k["oc1"]), _ptr(k["oc2"]), ch5, ch3, _ptr(k["tir"]), _ptr(k["gap"]), nl, nx, ny)
+        h = _vp()
+        check(L.wgrt_scene_create(ctypes.byref(desc), int(device), ctypes.byref(h)), "wgrt_scene_create")
+        self._h = h
+        self.device = int(device)
+        self.num_lmd, self.nx, self.ny = nl, nx, ny
+        self.n_fc_slices, self.n_oc_slices = nfc, noc
+        self.n_g = float(n_g)
+
+    @classmethod
+    def from_geometry(cls, geom, luts: dict, device: int = 0):
+        return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
+                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts["lut_ic1"], luts["lut_ic2"],
+                   luts["lut_ic3"], luts["lut_fc1"], luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"],
+                   geom.lut_TIR, geom.lut_gap, device=device)
+
+    @property
+    def handle(self):
+        if self._h is None:
+            raise WgrtError("scene destroyed")
+        return self._h
+
+    def info(self) -> dict:
+        inf = SceneInfo()
+        check(load().wgrt_scene_get_info(self.handle, ctypes.byref(inf)), "wgrt_scene_get_info")
+        return {f: getattr(inf, f) for f, _ in SceneInfo._fields_}
+
+    def eb_shape(self):
+        return (self.num_lmd, self.ny, self.nx, 80, 120)
+
+    def close(self):
+        if getattr(self, "_h", None) is not None:
+            load().wgrt_scene_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass

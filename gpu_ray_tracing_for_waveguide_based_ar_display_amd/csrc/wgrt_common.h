@@ -1,0 +1,127 @@
+// wgrt_common.h -- arithmetic shared by the device kernels and the host-side scene builder.
+//
+// Every function here is written with IEEE basic operations (+ - * / sqrt fma),
+// so a host and a device evaluation are bit-identical when compiled with
+// -ffp-contract=off (the build does).  Each one restates a device function of
+// the reference kernel module GPU_ray_tracing_functions.py (GRTF).
+#pragma once
+
+#include <stdint.h>
+
+#if defined(__HIPCC__)
+#include <hip/hip_runtime.h>
+#define WGRT_HD __host__ __device__ __forceinline__
+#else
+#include <cmath>
+#define WGRT_HD inline
+#endif
+
+namespace wgrt {
+
+#if !defined(__HIPCC__)
+using std::fabs;
+using std::floor;
+using std::fma;
+using std::frexp;
+using std::isinf;
+using std::isnan;
+using std::ldexp;
+using std::sqrt;
+#endif
+
+constexpr double kPi = 3.141592653589793;
+constexpr int kEbNy = 80;     // eyebox grid rows    (MAIN:37)
+constexpr int kEbNx = 120;    // eyebox grid columns (MAIN:37)
+constexpr double kOnEdgeTol = 1e-12;   // GRTF:68
+constexpr int64_t kMaxLoop = 100000;   // range(1e5), GRTF:905
+
+// ---------------------------------------------------------------------------
+// Packed per-(lambda, m, n) tile, in doubles.  Interaction "blocks" hold, for one
+// FSM state (and one coupler slice), the numerator cosines of the branch
+// efficiencies and the four complex Jones coefficients of every E_field_cal call in
+// the reference's argument order (p, q, r, s) -- see GRTF:860-1200.
+// ---------------------------------------------------------------------------
+constexpr int kTileTir = 0;       // lut_TIR[4]
+constexpr int kTileGap = 4;       // lut_gap[8]
+constexpr int kTileEbRange = 12;  // eff_reg_FOV_range[m, n, 4]
+constexpr int kTileEbRect = 16;   // eff_reg_FOV[m, n, 4, 2]
+constexpr int kTileCosIc1 = 24;   // cos(lut_ic1[l, m, n, 0].real)
+constexpr int kTileHeader = 28;
+constexpr int kBlock = 28;        // cosA[3], pad, rec[3][8]
+constexpr int kBlockCos = 0;
+constexpr int kBlockRec = 4;
+// block index: 0 in-coupling, 1 R0, 2 R1, 3 + k R2 slice k, 3 + nfc + k R3,
+//              3 + 2 nfc + k R4, 3 + 2 nfc + noc + k R5
+WGRT_HD int tile_doubles(int nfc, int noc) { return kTileHeader + kBlock * (3 + 2 * nfc + 2 * noc); }
+
+// ---------------------------------------------------------------------------
+// Correctly rounded hypot.  CPython 3.10's math.hypot (what the reference calls,
+// GRTF:145-146) is correctly rounded; so is this: exact double-double square sum
+// (FMA error terms) followed by one Newton correction of the square root.
+// ---------------------------------------------------------------------------
+WGRT_HD double hypot_cr(double x, double y) {
+    double ax = fabs(x), ay = fabs(y);
+    if (isinf(ax) || isinf(ay)) return INFINITY;
+    if (isnan(ax) || isnan(ay)) return NAN;
+    if (ax < ay) { double t = ax; ax = ay; ay = t; }
+    if (ay == 0.0) return ax;
+    int e;
+    (void)frexp(ax, &e);
+    const double sx = ldexp(ax, -e), sy = ldexp(ay, -e);
+    const double h = sx * sx, hl = fma(sx, sx, -h);
+    const double k = sy * sy, kl = fma(sy, sy, -k);
+    const double s = h + k;
+    const double lo = ((h - s) + k) + (hl + kl);
+    double r = sqrt(s);
+    const double rr = fma(-r, r, s);
+    r = r + (rr + lo) / (2.0 * r);
+    return ldexp(r, e);
+}
+
+// GRTF:124-130
+WGRT_HD double wrap_pi(double x) {
+    const double two_pi = 2.0 * kPi;
+    x = x + kPi;
+    x = x - two_pi * floor(x / two_pi);
+    return x - kPi;
+}
+
+// GRTF:52-61 + GRTF:36-50 fused into one edge pass.  The reference makes an
+// on-edge pass and then a crossing pass; both are order-independent (an "any" and
+// a parity), so one pass over the edges gives the identical result.
+WGRT_HD bool on_segment(double px, double py, double x1, double y1, double x2, double y2) {
+    const double lo_x = (x2 < x1 ? x2 : x1), hi_x = (x2 > x1 ? x2 : x1);
+    const double lo_y = (y2 < y1 ? y2 : y1), hi_y = (y2 > y1 ? y2 : y1);
+    if (px < lo_x - kOnEdgeTol || px > hi_x + kOnEdgeTol || py < lo_y - kOnEdgeTol ||
+        py > hi_y + kOnEdgeTol)
+        return false;
+    return fabs((x2 - x1) * (py - y1) - (y2 - y1) * (px - x1)) <= kOnEdgeTol;
+}
+
+// is_inside_or_on_edge(px, py, poly, 0, nv) (GRTF:63-71); xy = [nv][2]
+WGRT_HD bool inside_or_on_edge(double px, double py, const double *xy, int nv) {
+    bool inside = false;
+    int j = nv - 1;
+    for (int i = 0; i < nv; ++i) {
+        const double xi = xy[2 * i], yi = xy[2 * i + 1];
+        const double xj = xy[2 * j], yj = xy[2 * j + 1];
+        if (on_segment(px, py, xj, yj, xi, yi)) return true;
+        if (((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi + 1e-20) + xi))
+            inside = !inside;
+        j = i;
+    }
+    return inside;
+}
+
+// xorshift32 (13, 17, 5) of GRTF:25-34; gid is the GLOBAL ray index.
+WGRT_HD double rng_draw(uint32_t &s, int64_t gid) {
+    uint32_t v = s;
+    if (v == 0u) v = 0x6D2B79F5u ^ (uint32_t)(gid + 1);
+    v ^= v << 13;
+    v ^= v >> 17;
+    v ^= v << 5;
+    s = v;
+    return (double)v * (1.0 / 4294967296.0);
+}
+
+}  // namespace wgrt

@@ -1,0 +1,32 @@
+// wgrt_scene_build.h -- host-side scene preparation (see wgrt_scene_build.cpp).
+#pragma once
+
+#include <cstdint>
+#include <vector>
+
+#include "../../include/wgrt.h"
+
+namespace wgrt {
+
+struct LocatorHost {
+    std::vector<uint64_t> cells;   // [ncy][ncx], 2 bits per polygon: 0 OUT, 1 IN, 2 EDGE
+    std::vector<double> verts;     // all polygon vertices, [V][2]
+    std::vector<int32_t> poly_off; // polygon k = verts[poly_off[k] .. poly_off[k+1])
+    double x0 = 0, y0 = 0, h = 0, inv_h = 0;
+    int ncx = 0, ncy = 0;
+    int64_t edge_cells = 0;
+};
+
+struct SceneHost {
+    LocatorHost loc;
+    std::vector<double> tiles;     // [num_lmd * nx * ny][tile_doubles]
+    int tile_doubles = 0;
+};
+
+void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                   double cell_mm, LocatorHost &out);
+void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles);
+void validate_desc(const wgrt_scene_desc &d);
+void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out);
+
+}  // namespace wgrt

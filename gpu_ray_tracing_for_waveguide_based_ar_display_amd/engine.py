@@ -1,0 +1,118 @@
+"""Device-side entry points over torch ROCm tensors (PyTorch is the memory/stream plumbing).
+
+``trace_fullcolor`` is one launch of the bounce kernel (the reference's
+``process_rays_kernel_pro_fullColor[blocks, 256](...)``, GRTF:833-1246) through the
+C ABI ``wgrt_trace_fullcolor_ex``; it validates every buffer and raises on misuse
+instead of corrupting memory.
+"""
+from __future__ import annotations
+
+import ctypes
+
+import numpy as np
+import torch
+
+from . import _lib
+from ._lib import Rays, Scene, TraceStats, WgrtError, check, load
+
+RAY_COLUMNS = ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te", "tm", "delta_phase")
+READ_COLUMNS = ("x", "y", "m", "n", "lmd_num", "te", "tm", "delta_phase")
+
+VARIANT_AUTO, VARIANT_GRID, VARIANT_PERSISTENT = 0, 1, 2
+
+
+def _stream_handle(device: torch.device, stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream(device)
+    return int(s.cuda_stream)
+
+
+def _as_dev(t, dtype, name, device, n=None):
+    if not isinstance(t, torch.Tensor):
+        raise TypeError(f"{name} must be a torch tensor, got {type(t).__name__}")
+    if t.device != device:
+        raise ValueError(f"{name} is on {t.device}, expected {device}")
+    if t.dtype != dtype:
+        raise TypeError(f"{name} must be {dtype}, got {t.dtype}")
+    if not t.is_contiguous():
+        raise ValueError(f"{name} must be contiguous")
+    if n is not None and t.numel() != n:
+        raise ValueError(f"{name} has {t.numel()} elements, expected {n}")
+    return t
+
+
+def rays_to_device(rays: dict, device="cuda") -> dict:
+    """Copy the twelve float32 host columns (rays.build_rays) to device tensors."""
+    return {k: torch.from_numpy(np.ascontiguousarray(rays[k], dtype=np.float32)).to(device)
+            for k in RAY_COLUMNS if k in rays}
+
+
+def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
+                    gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
+                    per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
+                    workgroups: int = 0) -> None:
+    """Asynchronous launch on ``stream`` (default: torch's current stream).
+
+    rays: dict of device float32 tensors keyed like the reference columns
+    (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
+    kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
+    accepted too.  stats: optional int64[4] device tensor that is added to
+    (bounces, bad_rays, eyebox_hits, reserved).
+    """
+    device = torch.device("cuda", scene.device)
+    x = rays["x"]
+    N = x.numel() if n_rays is None else int(n_rays)
+    if N < 0 or N > x.numel():
+        raise ValueError(f"n_rays={N} out of range for {x.numel()} rays")
+    cols = {}
+    for k in READ_COLUMNS:
+        if k not in rays:
+            raise ValueError(f"missing ray column {k!r}")
+        cols[k] = _as_dev(rays[k], torch.float32, k, device, x.numel())
+    if rng_states.dtype not in (torch.int32, torch.uint32):
+        raise TypeError(f"rng_states must be uint32 (or an int32 view), got {rng_states.dtype}")
+    _as_dev(rng_states, rng_states.dtype, "rng_states", device, x.numel())
+    _as_dev(matrix_EB, torch.float32, "matrix_EB", device)
+    if tuple(matrix_EB.shape) != scene.eb_shape():
+        raise ValueError(f"matrix_EB shape {tuple(matrix_EB.shape)} != {scene.eb_shape()}")
+    if stats is not None:
+        _as_dev(stats, torch.int64, "stats", device, 4)
+    if per_ray_bounces is not None:
+        if per_ray_bounces.dtype not in (torch.int32, torch.uint32):
+            raise TypeError("per_ray_bounces must be uint32 / int32")
+        _as_dev(per_ray_bounces, per_ray_bounces.dtype, "per_ray_bounces", device, x.numel())
+    r = Rays(**{k: ctypes.c_void_p(cols[k].data_ptr()) for k in READ_COLUMNS})
+    for k in ("gap_x", "gap_y", "pol", "azi"):
+        setattr(r, k, ctypes.c_void_p(rays[k].data_ptr()) if k in rays else None)
+    check(load().wgrt_trace_fullcolor_ex(
+        scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
+        ctypes.c_void_p(matrix_EB.data_ptr()),
+        ctypes.c_void_p(stats.data_ptr()) if stats is not None else None,
+        ctypes.c_void_p(per_ray_bounces.data_ptr()) if per_ray_bounces is not None else None,
+        ctypes.c_void_p(_stream_handle(device, stream)), int(variant), int(workgroups)),
+        "wgrt_trace_fullcolor")
+
+
+def classify_points(scene: Scene, xy: torch.Tensor, stream=None) -> torch.Tensor:
+    """Per-point polygon membership bitmask through the scene's exact locator."""
+    device = torch.device("cuda", scene.device)
+    xy = _as_dev(xy, torch.float64, "xy", device)
+    n = xy.shape[0]
+    out = torch.empty(n, dtype=torch.int64, device=device)
+    check(load().wgrt_scene_classify(scene.handle, ctypes.c_void_p(xy.data_ptr()), n,
+                                     ctypes.c_void_p(out.data_ptr()),
+                                     ctypes.c_void_p(_stream_handle(device, stream))), "wgrt_scene_classify")
+    return out
+
+
+def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor:
+    """Device sqrt, div, hypot_cr, atan2, sin, cos, wrap on (a, b) -> [7, n] float64."""
+    n = a.numel()
+    out = torch.empty((7, n), dtype=torch.float64, device=a.device)
+    check(load().wgrt_selftest_math(ctypes.c_void_p(a.data_ptr()), ctypes.c_void_p(b.data_ptr()), n,
+                                    ctypes.c_void_p(out.data_ptr()),
+                                    ctypes.c_void_p(_stream_handle(a.device, stream))), "wgrt_selftest_math")
+    return out
+
+
+__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "rays_to_device", "classify_points",
+           "selftest_math", "RAY_COLUMNS", "_lib"]

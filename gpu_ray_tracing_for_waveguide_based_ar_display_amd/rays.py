@@ -51,12 +51,15 @@ def rng_seeds(n_rays: int, gid_offset: int = 0) -> np.ndarray:
     return ((gid + 1) * np.uint64(0x9E3779B9) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
 
 
-def build_rays(points: np.ndarray, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int):
+def build_rays(points: np.ndarray, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int,
+               blocks: tuple | None = None):
     """Twelve float32 SoA columns in the reference's block order (MAIN:65-115).
 
     ``points`` holds the ``rays_per_fov // 2`` origins shared by every block;
     ``lambdas`` lists the wavelength indices traced (``[0, 1, 2]`` full colour,
-    ``[1]`` for the single-lambda 532 nm configs).
+    ``[1]`` for the single-lambda 532 nm configs).  ``blocks = (lo, hi)`` builds only
+    FoV x wavelength blocks ``[lo, hi)`` -- global rays ``[lo * R, hi * R)`` -- which
+    is one rank's shard.
     """
     R = int(rays_per_fov)
     half = R // 2
@@ -65,11 +68,15 @@ def build_rays(points: np.ndarray, num_fov_x: int, num_fov_y: int, lambdas, rays
         raise ValueError(f"points must have shape ({half}, 2), got {pts.shape}")
     lam = np.asarray(list(lambdas), dtype=np.float32)
     nl = len(lam)
-    nblk = num_fov_x * num_fov_y * nl
+    nblk_all = num_fov_x * num_fov_y * nl
+    lo, hi = (0, nblk_all) if blocks is None else (int(blocks[0]), int(blocks[1]))
+    if not 0 <= lo <= hi <= nblk_all:
+        raise ValueError(f"block range {blocks} outside [0, {nblk_all}]")
+    nblk = hi - lo
     N = nblk * R
     ii, jj, ll = np.meshgrid(np.arange(num_fov_x, dtype=np.float32),
                              np.arange(num_fov_y, dtype=np.float32), lam, indexing="ij")
-    per_ray = lambda v: np.repeat(v.reshape(-1), R)
+    per_ray = lambda v: np.repeat(v.reshape(-1)[lo:hi], R)
     r = np.arange(N) % R
     te_half = r < half
     origin = np.tile(np.concatenate([pts, pts]).astype(np.float32), (nblk, 1))

@@ -1,0 +1,148 @@
+/*
+ * wgrt.h -- C ABI of the MI355X waveguide ray-tracing engine (libwgrt.so).
+ *
+ * Drop-in boundary for the reference's hot path, the Numba kernel call
+ *
+ *   process_rays_kernel_pro_fullColor[blocks, threads](
+ *       x_v, y_v, gap_x_v, gap_y_v, pol_v, azi_v, m_v, n_v, lmd_num, te_v, tm_v, delta_phase_v,
+ *       rng_states, IC, FC, FC_offset, OC, OC_offset, n_g,
+ *       eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
+ *       lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2, lut_TIR, lut_gap, matrix_EB)
+ *
+ * (reference GPU_ray_tracing_functions.py:833-841, launched at
+ * gpu_ray_tracing_pro_fullColor.py:169-177).  The 33 arguments split into
+ *   - the scene (geometry + LUTs, 19 arguments, constant across launches):
+ *       wgrt_scene_create()  -- replaces the cuda.to_device uploads at MAIN:40-57
+ *   - the per-launch ray batch, RNG state and eyebox grid (14 arguments):
+ *       wgrt_trace_fullcolor() -- replaces one kernel launch (MAIN:170)
+ *
+ * Conventions (same as the reference's): the caller owns every buffer; the
+ * trace call allocates nothing, accumulates into matrix_EB (never zeroes it),
+ * mutates rng_states, leaves the ray arrays untouched, and is asynchronous on
+ * the given HIP stream (the caller synchronises, MAIN:178).  Differences: every
+ * entry point validates its arguments and returns a wgrt_status instead of
+ * silently corrupting memory; out-of-range m / n / lmd_num rays are skipped
+ * and counted (wgrt_trace_stats.bad_rays) rather than read out of bounds.
+ *
+ * All pointers passed to wgrt_trace_* are DEVICE pointers (hipMalloc'd or torch
+ * ROCm tensors); all pointers in wgrt_scene_desc are HOST pointers.
+ */
+#ifndef WGRT_H
+#define WGRT_H
+
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define WGRT_ABI_VERSION 1
+
+typedef enum {
+    WGRT_OK = 0,
+    WGRT_ERR_INVALID_ARGUMENT = 1,
+    WGRT_ERR_HIP = 2,
+    WGRT_ERR_OUT_OF_MEMORY = 3,
+    WGRT_ERR_UNSUPPORTED = 4,
+} wgrt_status;
+
+/* Geometry + look-up tables, exactly the arrays couplers_coor_full_color() and the
+ * seven lut_*_fullColor.npy files provide (reference couplers_coor.py:740-750,
+ * gpu_ray_tracing_pro_fullColor.py:19-34).  Host pointers, C-contiguous. */
+typedef struct {
+    const double *IC;                 /* [n_ic, 2]                                   */
+    int64_t n_ic;
+    const double *FC;                 /* [FC_offset[n_fc_slices], 2]                  */
+    const int64_t *FC_offset;         /* [n_fc_slices + 1]                            */
+    int64_t n_fc_slices;
+    const double *OC;                 /* [OC_offset[n_oc_slices], 2]                  */
+    const int64_t *OC_offset;         /* [n_oc_slices + 1]                            */
+    int64_t n_oc_slices;
+    double n_g;                       /* substrate index                              */
+    const double *eff_reg1;           /* [n_eff_reg1, 2] whole effective region       */
+    int64_t n_eff_reg1;
+    const double *eff_reg2;           /* [n_eff_reg2, 2] IC+FC effective region       */
+    int64_t n_eff_reg2;
+    const double *eff_reg_FOV;        /* [nx, ny, 4, 2] per-FoV eyebox rectangle      */
+    const double *eff_reg_FOV_range;  /* [nx, ny, 4] = xmin, xmax, ymin, ymax         */
+    /* complex128 tables, interleaved (re, im); channel counts ch5 (>= 41), ch3 (>= 20) */
+    const double *lut_ic1, *lut_ic2, *lut_ic3;   /* [num_lmd, nx, ny, ch5]              */
+    const double *lut_fc1, *lut_fc2;             /* [n_fc_slices, num_lmd, nx, ny, ch3] */
+    const double *lut_oc1, *lut_oc2;             /* [n_oc_slices, num_lmd, nx, ny, ch5] */
+    int32_t ch5, ch3;
+    const double *lut_TIR;            /* [num_lmd, nx, ny, 4]                         */
+    const double *lut_gap;            /* [num_lmd, nx, ny, 8]                         */
+    int32_t num_lmd, nx, ny;
+} wgrt_scene_desc;
+
+typedef struct wgrt_scene wgrt_scene;   /* opaque, device-resident */
+
+/* The twelve per-ray float32 columns of the reference (MAIN:65-76), device pointers.
+ * Columns the kernel never reads (gap_x, gap_y, pol, azi: overwritten before use at
+ * GRTF:872-894) may be NULL. */
+typedef struct {
+    const float *x, *y, *gap_x, *gap_y, *pol, *azi, *m, *n, *lmd_num, *te, *tm, *delta_phase;
+} wgrt_rays;
+
+typedef struct {
+    uint64_t bounces;      /* ray-bounce events: 1 in-coupling + loop iterations, per ray */
+    uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num               */
+    uint64_t eyebox_hits;  /* rays accumulated into matrix_EB                             */
+    uint64_t reserved;
+} wgrt_trace_stats;
+
+typedef struct {
+    int64_t tile_bytes;        /* packed per-(lambda, FoV) LUT tile                   */
+    int64_t tiles;             /* num_lmd * nx * ny                                   */
+    int64_t grid_cells_x, grid_cells_y;
+    double grid_cell_mm;
+    int64_t grid_edge_cells;   /* cells whose class needs the exact polygon test      */
+    int32_t n_polygons;
+    int32_t device;
+} wgrt_scene_info;
+
+/* Build the device-resident scene (packs LUT tiles, builds the exact polygon
+ * locator) on HIP device `device`.  Replaces MAIN:40-57. */
+wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scene **out);
+wgrt_status wgrt_scene_destroy(wgrt_scene *scene);
+wgrt_status wgrt_scene_get_info(const wgrt_scene *scene, wgrt_scene_info *info);
+
+/* One launch of the full-colour bounce kernel over rays [0, n_rays) whose global
+ * ray index is gid_offset + i (gid seeds the zero-state RNG fix-up, GRTF:28-29, and
+ * keeps results independent of sharding).  rng_states[n_rays] is read and written;
+ * matrix_EB [num_lmd, ny, nx, 80, 120] float32 is accumulated into.
+ *   stats:          optional DEVICE pointer to a wgrt_trace_stats that is ADDED to
+ *                   (zero it yourself);
+ *   per_ray_bounces: optional DEVICE uint32[n_rays] of per-ray bounce counts;
+ *   stream:         hipStream_t (NULL = default stream).
+ * Replaces gpu_ray_tracing_pro_fullColor.py:170 (GRTF:833-1246). */
+wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
+                                 int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
+                                 wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream);
+
+/* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
+ * count for the persistent variant (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
+ * grid, 2 persistent wave-refill. */
+wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
+                                    int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
+                                    wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
+                                    int variant, int workgroups);
+
+/* Polygon membership of n points (DEVICE xy[n, 2]) through the scene's locator:
+ * bit k of out_mask[i] = is_inside_or_on_edge(point i, polygon k) with polygon order
+ * 0 eff_reg1, 1 eff_reg2, 2 IC, 3.. FC slices, then OC slices (GRTF:63-71).  Test hook. */
+wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64_t n,
+                                uint64_t *out_mask, void *stream);
+
+/* Device math self-test (test hook): for i < n, out[k * n + i] holds
+ * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */
+wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, double *out, void *stream);
+
+const char *wgrt_status_string(wgrt_status s);
+const char *wgrt_last_error(void);   /* detail of the last failure on this thread */
+int wgrt_abi_version(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* WGRT_H */

@@ -76,8 +76,21 @@ def lib():
         L.wgrt_oracle_inside.argtypes = [ctypes.c_double, ctypes.c_double, _f64p, ctypes.c_int64]
         L.wgrt_oracle_xorshift.restype = ctypes.c_uint32
         L.wgrt_oracle_xorshift.argtypes = [ctypes.c_uint32, ctypes.c_int64, _f64p]
+        L.wgrt_oracle_inside_many.restype = None
+        L.wgrt_oracle_inside_many.argtypes = [_f64p, ctypes.c_int64, _f64p, ctypes.c_int64,
+                                              ctypes.POINTER(ctypes.c_int32)]
         _lib = L
     return _lib
+
+
+def inside_many(points: np.ndarray, poly: np.ndarray) -> np.ndarray:
+    """Reference predicate is_inside_or_on_edge (GRTF:63-71) for many points."""
+    pts = np.ascontiguousarray(points, dtype=np.float64)
+    P = np.ascontiguousarray(poly, dtype=np.float64)
+    out = np.zeros(pts.shape[0], dtype=np.int32)
+    lib().wgrt_oracle_inside_many(pts.ctypes.data_as(_f64p), pts.shape[0], P.ctypes.data_as(_f64p),
+                                  P.shape[0], out.ctypes.data_as(ctypes.POINTER(ctypes.c_int32)))
+    return out
 
 
 def _p(a, t):

@@ -408,3 +408,8 @@ uint32_t wgrt_oracle_xorshift(uint32_t s, int64_t gid, double *u) {
     *u = rng_draw(&s, gid);
     return s;
 }
+
+void wgrt_oracle_inside_many(const double *pts, int64_t n, const double *xy, int64_t nv, int32_t *out) {
+#pragma omp parallel for schedule(static)
+    for (int64_t i = 0; i < n; ++i) out[i] = inside_or_on_edge(pts[2 * i], pts[2 * i + 1], xy, nv);
+}

@@ -44,6 +44,7 @@ double wgrt_oracle_hypot(double x, double y);
 double wgrt_oracle_wrap(double x);
 int wgrt_oracle_inside(double px, double py, const double *xy, int64_t nv);
 uint32_t wgrt_oracle_xorshift(uint32_t s, int64_t gid, double *u);
+void wgrt_oracle_inside_many(const double *pts, int64_t n, const double *xy, int64_t nv, int32_t *out);
 
 #ifdef __cplusplus
 }

@@ -1,0 +1,86 @@
+"""CPU-side checks of the C ABI (no kernel launches): the library loads, exports every
+symbol include/wgrt.h declares, and rejects malformed scenes before touching the GPU."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def declared_symbols():
+    text = open(os.path.join(REPO, "include", "wgrt.h")).read()
+    text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
+    return sorted(set(re.findall(r"\b(wgrt_[a-z0-9_]+)\s*\(", text)))
+
+
+@pytest.fixture(scope="module")
+def lib():
+    if not os.path.exists(_lib.LIB_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return _lib.load()
+
+
+def test_header_declares_the_bound_symbols():
+    assert declared_symbols() == sorted(_lib.EXPORTED)
+
+
+def test_library_exports_every_declared_symbol(lib):
+    for name in declared_symbols():
+        assert hasattr(lib, name), name
+
+
+def test_abi_version_and_status_strings(lib):
+    assert lib.wgrt_abi_version() == _lib.ABI_VERSION
+    assert lib.wgrt_status_string(0) == b"ok"
+    assert lib.wgrt_status_string(1) == b"invalid argument"
+
+
+def _desc_from(geom, luts, **over):
+    keep = []
+
+    def p(a, t=np.float64, ct=ctypes.c_double):
+        a = np.ascontiguousarray(a, dtype=t)
+        keep.append(a)
+        return a.ctypes.data_as(ctypes.POINTER(ct))
+    d = _lib.SceneDesc(
+        p(geom.IC), len(geom.IC), p(geom.FC), p(geom.FC_offset, np.int64, ctypes.c_int64),
+        len(geom.FC_offset) - 1, p(geom.OC), p(geom.OC_offset, np.int64, ctypes.c_int64),
+        len(geom.OC_offset) - 1, geom.n_g, p(geom.eff_reg1), len(geom.eff_reg1), p(geom.eff_reg2),
+        len(geom.eff_reg2), p(geom.eff_reg_FOV), p(geom.eff_reg_FOV_range),
+        *[p(luts[k], np.complex128) for k in ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1", "lut_fc2",
+                                              "lut_oc1", "lut_oc2")],
+        42, 26, p(geom.lut_TIR), p(geom.lut_gap), 3, geom.eff_reg_FOV.shape[0], geom.eff_reg_FOV.shape[1])
+    for k, v in over.items():
+        setattr(d, k, v)
+    return d, keep
+
+
+@pytest.mark.parametrize("field,value,msg", [
+    ("ch5", 30, b"channels"),
+    ("ch3", 10, b"channels"),
+    ("nx", 0, b"positive"),
+    ("n_fc_slices", 40, b"too many"),
+    ("lut_TIR", None, b"NULL"),
+])
+def test_scene_create_validates_before_gpu(lib, field, value, msg):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    g = design_geometry(3, 3)
+    L = synthetic_luts(g)
+    d, keep = _desc_from(g, L, **{field: value})
+    h = ctypes.c_void_p()
+    st = lib.wgrt_scene_create(ctypes.byref(d), 0, ctypes.byref(h))
+    assert st == 1
+    assert msg in lib.wgrt_last_error()
+    assert not h.value
+
+
+def test_trace_rejects_null_scene(lib):
+    r = _lib.Rays()
+    assert lib.wgrt_trace_fullcolor(None, ctypes.byref(r), 10, 0, None, None, None, None, None) == 1

@@ -1,0 +1,34 @@
+#!/bin/bash
+# One GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
+# Stops at the first step that dies abnormally (fault / abort / timeout); plain test
+# failures (pytest exit 1) are recorded and the later steps still run.
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+ROOT=$(pwd)
+OUT=$ROOT/gpurun_out
+mkdir -p "$OUT"
+export TMPDIR=/tmp
+ok_or_stop() {  # $1 = exit code, $2 = step name
+  local rc=$1
+  echo "[$2] exit $rc" | tee -a "$OUT/steps.log"
+  if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after abnormal exit of $2"; exit "$rc"; fi
+}
+STEPS=${STEPS:-pytest,smoke,bench,prof}
+if [[ $STEPS == *pytest* ]]; then
+  timeout -k 10 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  ok_or_stop $? pytest
+fi
+if [[ $STEPS == *smoke* ]]; then
+  timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
+  ok_or_stop $? smoke
+fi
+if [[ $STEPS == *bench* ]]; then
+  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
+  ok_or_stop $? bench
+fi
+if [[ $STEPS == *prof* ]]; then
+  cd /tmp
+  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1
+  ok_or_stop $? prof
+fi
+exit 0
