@@ -65,6 +65,17 @@ WGRT_HD double hypot_cr(double x, double y) {
     if (isnan(ax) || isnan(ay)) return NAN;
     if (ax < ay) { double t = ax; ax = ay; ay = t; }
     if (ay == 0.0) return ax;
+    if (ax <= 0x1p400 && ay >= 0x1p-400) {
+        // No scaling needed: every intermediate below stays normal, so the result is
+        // bit-identical to the power-of-two-scaled evaluation (rounding is scale-invariant).
+        const double h = ax * ax, hl = fma(ax, ax, -h);
+        const double k = ay * ay, kl = fma(ay, ay, -k);
+        const double s = h + k;
+        const double lo = ((h - s) + k) + (hl + kl);
+        double r = sqrt(s);
+        const double rr = fma(-r, r, s);
+        return r + (rr + lo) / (2.0 * r);
+    }
     int e;
     (void)frexp(ax, &e);
     const double sx = ldexp(ax, -e), sy = ldexp(ay, -e);
@@ -109,6 +120,25 @@ WGRT_HD bool inside_or_on_edge(double px, double py, const double *xy, int nv) {
         if (((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi + 1e-20) + xi))
             inside = !inside;
         j = i;
+    }
+    return inside;
+}
+
+// The same predicate over a subset of the polygon's edges (edge = end-vertex index i,
+// start vertex i - 1 mod nv).  Equal to inside_or_on_edge whenever the omitted edges can
+// neither pass on_segment's bounding-box check nor straddle py (see the row-band lists in
+// wgrt_scene_build.cpp).
+WGRT_HD bool inside_or_on_edge_subset(double px, double py, const double *xy, int nv,
+                                      const int32_t *edges, int ne) {
+    bool inside = false;
+    for (int e = 0; e < ne; ++e) {
+        const int i = edges[e];
+        const int j = (i == 0) ? nv - 1 : i - 1;
+        const double xi = xy[2 * i], yi = xy[2 * i + 1];
+        const double xj = xy[2 * j], yj = xy[2 * j + 1];
+        if (on_segment(px, py, xj, yj, xi, yi)) return true;
+        if (((yi > py) != (yj > py)) && (px < (xj - xi) * (py - yi) / (yj - yi + 1e-20) + xi))
+            inside = !inside;
     }
     return inside;
 }

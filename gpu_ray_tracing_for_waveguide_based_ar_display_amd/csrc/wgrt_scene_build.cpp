@@ -19,7 +19,10 @@
 //     every point gives the same answer as the centre, bit for bit: the on-edge test
 //     fails on its bounding-box pre-check or on |cross| > tol (|edge| * kPad >> tol),
 //     and each crossing comparison is at least kPad from its rounding-sensitive point.
-//     EDGE cells fall back to the exact per-edge test in the kernel.
+//     EDGE cells fall back to the exact reference predicate in the kernel, restricted to
+//     the polygon's edges whose (padded) y-range meets the cell's row: every other edge
+//     fails on_segment's y bounding-box check and cannot straddle the point's y, so
+//     dropping it changes neither the "any on-edge" nor the crossing parity.
 #include <algorithm>
 #include <cmath>
 #include <cstdint>
@@ -116,6 +119,21 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
     out.edge_cells = 0;
 
     std::vector<uint8_t> edge((size_t)ncx * ncy);
+    out.row_off.assign((size_t)np * ncy + 1, 0);
+    out.row_edges.clear();
+    for (int k = 0; k < np; ++k) {
+        const double *xy = polys[k];
+        const int64_t nv = nverts[k];
+        for (int cy = 0; cy < ncy; ++cy) {
+            const double by0 = y0 + cy * h - 2 * kPad, by1 = y0 + (cy + 1) * h + 2 * kPad;
+            for (int64_t i = 0, j = nv - 1; i < nv; j = i++) {
+                const double ey0 = std::min(xy[2 * j + 1], xy[2 * i + 1]) - 2 * kPad;
+                const double ey1 = std::max(xy[2 * j + 1], xy[2 * i + 1]) + 2 * kPad;
+                if (!(ey1 < by0 || ey0 > by1)) out.row_edges.push_back((int32_t)i);
+            }
+            out.row_off[(size_t)k * ncy + cy + 1] = (int32_t)out.row_edges.size();
+        }
+    }
     for (int k = 0; k < np; ++k) {
         std::fill(edge.begin(), edge.end(), 0);
         const double *xy = polys[k];

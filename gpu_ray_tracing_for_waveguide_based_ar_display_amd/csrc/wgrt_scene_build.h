@@ -12,6 +12,11 @@ struct LocatorHost {
     std::vector<uint64_t> cells;   // [ncy][ncx], 2 bits per polygon: 0 OUT, 1 IN, 2 EDGE
     std::vector<double> verts;     // all polygon vertices, [V][2]
     std::vector<int32_t> poly_off; // polygon k = verts[poly_off[k] .. poly_off[k+1])
+    // row-band edge lists (CSR): the edges of polygon k whose y-range, padded, meets cell
+    // row cy are row_edges[row_off[k * ncy + cy] .. row_off[k * ncy + cy + 1]), each given
+    // as the index i (within polygon k) of its end vertex; its start vertex is i - 1 (mod nv)
+    std::vector<int32_t> row_off;
+    std::vector<int32_t> row_edges;
     double x0 = 0, y0 = 0, h = 0, inv_h = 0;
     int ncx = 0, ncy = 0;
     int64_t edge_cells = 0;

@@ -26,6 +26,7 @@
 
 #include <cstdio>
 #include <cstring>
+#include <atomic>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -59,6 +60,8 @@ struct Locator {
     const uint64_t *cells;
     const double *verts;
     const int32_t *poly_off;
+    const int32_t *row_off;
+    const int32_t *row_edges;
     double x0, y0, inv_h;
     int ncx, ncy;
 };
@@ -81,39 +84,60 @@ constexpr int kPolyEff2 = 1;
 constexpr int kPolyIC = 2;
 constexpr int kPolyFC0 = 3;
 
-__device__ __forceinline__ uint64_t cell_word(const Locator &L, double x, double y) {
+// A point's cell of the locator grid: the per-polygon class word and the cell row.
+struct Cell {
+    uint64_t w;
+    int cy;
+};
+
+__device__ __forceinline__ Cell locate(const Locator &L, double x, double y) {
     const double fx = floor((x - L.x0) * L.inv_h);
     const double fy = floor((y - L.y0) * L.inv_h);
     // NaN / out-of-grid points are outside every polygon (cell word 0 = all OUT)
-    if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return 0ull;
-    return L.cells[(int)fy * L.ncx + (int)fx];
+    if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return Cell{0ull, 0};
+    const int cx = (int)fx, cy = (int)fy;
+    return Cell{L.cells[cy * L.ncx + cx], cy};
 }
 
-__device__ __forceinline__ bool in_poly(const Locator &L, uint64_t w, int k, double x, double y) {
-    const unsigned c = (unsigned)(w >> (2 * k)) & 3u;
-    if (c != 2u) return c == 1u;
-    const int a = L.poly_off[k], b = L.poly_off[k + 1];
-    return inside_or_on_edge(x, y, L.verts + 2 * a, b - a);
+// is_inside_or_on_edge(x, y, polygon k) (GRTF:63-71): the cell class when the cell is IN or
+// OUT, else the reference predicate over the polygon's edges that meet the cell's row.
+__device__ __forceinline__ bool in_poly(const Locator &L, const Cell &c, int k, double x, double y) {
+    const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
+    if (cls != 2u) return cls == 1u;
+    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
+    const int r = k * L.ncy + c.cy;
+    const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
+    return inside_or_on_edge_subset(x, y, L.verts + 2 * a, nv, L.row_edges + e0, e1 - e0);
 }
 
-// First slice s in [first, first + count) containing (x, y), -1 if none (GRTF:1002-1005).
-__device__ __forceinline__ int first_slice(const Locator &L, uint64_t w, int first, int count,
+// First slice s in [0, count) of polygons first .. first + count - 1 containing (x, y),
+// -1 if none (the slice scans of GRTF:1002-1005 and GRTF:1112-1115, which stop at the
+// first hit).  Candidates come straight from the cell word: a slice is tested exactly only
+// when its class is EDGE; an IN slice is a hit; OUT slices are skipped.
+__device__ __forceinline__ int first_slice(const Locator &L, const Cell &c, int first, int count,
                                            double x, double y) {
-    for (int s = 0; s < count; ++s)
-        if (in_poly(L, w, first + s, x, y)) return s;
+    uint64_t f = c.w >> (2 * first);
+    if (count < 32) f &= (1ull << (2 * count)) - 1ull;
+    const uint64_t in = f & 0x5555555555555555ull;           // class 01
+    uint64_t cand = in | ((f >> 1) & 0x5555555555555555ull);  // class 01 or 10
+    while (cand != 0ull) {
+        const int p = __builtin_ctzll(cand);
+        const int s = p >> 1;
+        if ((in >> p) & 1ull) return s;
+        if (in_poly(L, c, first + s, x, y)) return s;
+        cand &= cand - 1ull;
+    }
     return -1;
 }
 
-struct Amp {
-    double te_re, te_im, tm_re, tm_im, te, tm;
+// E_field_cal (GRTF:132-152).  rec = (p, q, r, s) complex in the reference call's argument
+// order: Ete' = p*te_in + r*tm_in, Etm' = q*te_in + s*tm_in.  The multiplications by 0.0 are
+// Python's real->complex promotions; they are kept so signed zeros propagate exactly.
+struct Field {
+    double te_re, te_im, tm_re, tm_im;
 };
 
-// E_field_cal (GRTF:132-152) up to the magnitudes.  rec = (p, q, r, s) complex, the
-// reference call's argument order: Ete' = p*te_in + r*tm_in, Etm' = q*te_in + s*tm_in.
-// The multiplications by 0.0 are Python's real->complex promotions; they are kept so
-// signed zeros propagate exactly as in the reference.
-__device__ __forceinline__ void efield_amp(double Ete, double Etm, double cd, double sd,
-                                           const double *rec, Amp &o) {
+__device__ __forceinline__ Field efield(double Ete, double Etm, double cd, double sd, const double *rec) {
     const double pr = rec[0], pi = rec[1], qr = rec[2], qi = rec[3];
     const double rr = rec[4], ri = rec[5], sr = rec[6], si = rec[7];
     const double ti_re = cd * Etm - sd * 0.0, ti_im = cd * 0.0 + sd * Etm;
@@ -121,17 +145,14 @@ __device__ __forceinline__ void efield_amp(double Ete, double Etm, double cd, do
     const double b_re = rr * ti_re - ri * ti_im, b_im = rr * ti_im + ri * ti_re;
     const double c_re = qr * Ete - qi * 0.0, c_im = qr * 0.0 + qi * Ete;
     const double d_re = sr * ti_re - si * ti_im, d_im = sr * ti_im + si * ti_re;
-    o.te_re = a_re + b_re;
-    o.te_im = a_im + b_im;
-    o.tm_re = c_re + d_re;
-    o.tm_im = c_im + d_im;
-    o.te = hypot_cr(o.te_re, o.te_im);
-    o.tm = hypot_cr(o.tm_re, o.tm_im);
+    return Field{a_re + b_re, a_im + b_im, c_re + d_re, c_im + d_im};
 }
 
-__device__ __forceinline__ double efield_phase(const Amp &o) {
-    const double pte = (o.te >= 1e-20) ? atan2(o.te_im, o.te_re) : 0.0;
-    const double ptm = (o.tm >= 1e-20) ? atan2(o.tm_im, o.tm_re) : 0.0;
+// Output phase difference of E_field_cal: wrap(atan2(Etm') - atan2(Ete')), 0 phase for a
+// component with |.| < 1e-20 (GRTF:147-150).
+__device__ __forceinline__ double efield_phase(const Field &f, double te, double tm) {
+    const double pte = (te >= 1e-20) ? atan2(f.te_im, f.te_re) : 0.0;
+    const double ptm = (tm >= 1e-20) ? atan2(f.tm_im, f.tm_re) : 0.0;
     return wrap_pi(ptm - pte);
 }
 
@@ -141,30 +162,81 @@ struct Ray {
     int region;
 };
 
+// One ray in flight on a lane.
+struct Lane {
+    Ray r;
+    const double *T;   // this ray's (lambda, m, n) tile
+    int64_t i;         // local ray index
+    int l, m, n;
+    uint32_t bounces;  // 1 in-coupling event + loop iterations (GRTF:905)
+    bool hit;          // accumulated into matrix_EB
+};
+
+// Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
+// FoV / wavelength indices fall outside the scene.
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L) {
+    const int m = (int)A.m[i], n = (int)A.n[i], l = (int)A.l[i];
+    if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
+    L.i = i;
+    L.l = l;
+    L.m = m;
+    L.n = n;
+    L.T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
+    L.r.x = (double)A.x[i];
+    L.r.y = (double)A.y[i];
+    L.r.te = (double)A.te[i];
+    L.r.tm = (double)A.tm[i];
+    L.r.dph = (double)A.dph[i];
+    L.r.cos_t = 1.0;
+    L.r.ener = 1.0;
+    L.r.s = A.rng[i];
+    L.r.region = 0;
+    L.bounces = 1;
+    L.hit = false;
+    return true;
+}
+
 enum : int { kDie = -1 };
 
-// kind: 0 in-coupler states (entry event, R0, R1), 1 R2, 2 R3, 3 R4, 4 R5.
-// Returns the next region or kDie; *eb_hit set when the ray is out-coupled into the eyebox.
-__device__ __forceinline__ int interact(const TraceArgs &A, Ray &r, const double *T, const double *B,
-                                        int kind, bool entry, int64_t gid, int l, int m, int n,
-                                        bool &eb_hit) {
+// A coupler interaction: `blk` of the lane's tile, `kind` 0 in-coupler states (entry event,
+// R0, R1), 1 R2, 2 R3, 3 R4, 4 R5.  Evaluates every branch's efficiency (GRTF:860-869,
+// 909-918, ..., 1186-1200), draws, and applies the chosen branch.  Returns the next region
+// or kDie.  Only the chosen branch's phase (two atan2) is evaluated; its field is recomputed
+// by the same operations rather than kept in registers for every branch.
+__device__ __forceinline__ int interact(const TraceArgs &A, Lane &L, int blk, int kind, bool entry) {
+    Ray &r = L.r;
+    const double *T = L.T;
+    const double *B = T + kTileHeader + kBlock * blk;
     double sd, cd;
     sincos(r.dph, &sd, &cd);
     const bool three = kind >= 3;
-    Amp a0, a1, a2;
-    efield_amp(r.te, r.tm, cd, sd, B + kBlockRec, a0);
-    efield_amp(r.te, r.tm, cd, sd, B + kBlockRec + 8, a1);
-    if (three) efield_amp(r.te, r.tm, cd, sd, B + kBlockRec + 16, a2);
     const double denom = entry ? T[kTileCosIc1] : r.cos_t;
-    double e0 = (a0.te * a0.te + a0.tm * a0.tm) * B[0] / denom;
-    double e1 = (a1.te * a1.te + a1.tm * a1.tm) * B[1] / denom;
+    double te[3], tm[3];
+    {
+        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec);
+        te[0] = hypot_cr(f.te_re, f.te_im);
+        tm[0] = hypot_cr(f.tm_re, f.tm_im);
+    }
+    {
+        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8);
+        te[1] = hypot_cr(f.te_re, f.te_im);
+        tm[1] = hypot_cr(f.tm_re, f.tm_im);
+    }
+    te[2] = tm[2] = 0.0;
+    if (three) {
+        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 16);
+        te[2] = hypot_cr(f.te_re, f.te_im);
+        tm[2] = hypot_cr(f.tm_re, f.tm_im);
+    }
+    double e0 = (te[0] * te[0] + tm[0] * tm[0]) * B[0] / denom;
+    double e1 = (te[1] * te[1] + tm[1] * tm[1]) * B[1] / denom;
     if (entry) {
         e0 = e0 * A.n_g;
         e1 = e1 * A.n_g;
     }
     double e2 = 0.0;
-    if (three) e2 = (a2.te * a2.te + a2.tm * a2.tm) * B[2] / denom / A.n_g;
-    const double u = rng_draw(r.s, gid);
+    if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
+    const double u = rng_draw(r.s, A.gid_offset + L.i);
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
     int b;
     if (u <= e0 && (!thr || r.ener * e0 > 0.0)) b = 0;
@@ -183,33 +255,35 @@ __device__ __forceinline__ int interact(const TraceArgs &A, Ray &r, const double
             // equal to the axis length aliases into the next row; guarded to the buffer
             if (ix < 0) ix += kEbNx;
             if (iy < 0) iy += kEbNy;
-            const int64_t off = ((((int64_t)l * A.ny + n) * A.nx + m) * kEbNy + iy) * kEbNx + ix;
+            const int64_t off = ((((int64_t)L.l * A.ny + L.n) * A.nx + L.m) * kEbNy + iy) * kEbNx + ix;
             const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
             if (off >= 0 && off < total) {
                 unsafeAtomicAdd(A.eb + off, 1.0f);
-                eb_hit = true;
+                L.hit = true;
             }
         }
         return kDie;
     }
-    const Amp &c = b == 0 ? a0 : a1;
+    const double cte = b == 0 ? te[0] : te[1];
+    const double ctm = b == 0 ? tm[0] : tm[1];
     const double e = b == 0 ? e0 : e1;
+    const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * b);
     // take the branch (GRTF:872-882 and every branch body after it)
-    const double norm = sqrt(c.te * c.te + c.tm * c.tm);
-    const double ph = efield_phase(c);
+    const double norm = sqrt(cte * cte + ctm * ctm);
+    const double ph = efield_phase(f, cte, ctm);
     int tir, gap;
     if (kind == 0) { tir = b == 0 ? 0 : 2; gap = b == 0 ? 0 : 4; }
     else if (kind <= 2) { tir = b == 0 ? 0 : 1; gap = b == 0 ? 0 : 2; }
     else { tir = b == 0 ? 1 : 3; gap = b == 0 ? 2 : 6; }
     r.cos_t = B[b];
-    r.te = c.te / norm;
-    r.tm = c.tm / norm;
+    r.te = cte / norm;
+    r.tm = ctm / norm;
     r.dph = ph + T[kTileTir + tir];
     r.x += T[kTileGap + gap];
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
     if (kind == 0) {
-        const bool in_ic = in_poly(A.loc, cell_word(A.loc, r.x, r.y), kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly(A.loc, locate(A.loc, r.x, r.y), kPolyIC, r.x, r.y);
         if (b == 0) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -217,80 +291,58 @@ __device__ __forceinline__ int interact(const TraceArgs &A, Ray &r, const double
     return b == 0 ? 4 : 5;
 }
 
-struct RayOutcome {
-    uint32_t bounces;
-    bool eb_hit;
-    bool bad;
-};
-
-__device__ __forceinline__ RayOutcome trace_one(const TraceArgs &A, int64_t i) {
-    RayOutcome out{0u, false, false};
-    const int m = (int)A.m[i], n = (int)A.n[i], l = (int)A.l[i];
-    if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) {
-        out.bad = true;
-        return out;
-    }
-    const int64_t gid = A.gid_offset + i;
-    const double *T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
-    const double *blocks = T + kTileHeader;
-    Ray r;
-    r.x = (double)A.x[i];
-    r.y = (double)A.y[i];
-    r.te = (double)A.te[i];
-    r.tm = (double)A.tm[i];
-    r.dph = (double)A.dph[i];
-    r.cos_t = 1.0;
-    r.ener = 1.0;
-    r.s = A.rng[i];
-    uint32_t bounces = 1;
-    bool hit = false;
-    int region = interact(A, r, T, blocks, 0, true, gid, l, m, n, hit);
-    const int nfc = A.nfc, noc = A.noc;
-    for (int64_t it = 0; region >= 0 && it < kMaxLoop; ++it) {
-        ++bounces;
-        const uint64_t w = cell_word(A.loc, r.x, r.y);
-        if (!in_poly(A.loc, w, kPolyEff1, r.x, r.y)) break;  // GRTF:906
-        int blk;
-        int kind;
+// Run a ray through the loop iterations that need no Monte-Carlo interaction -- hops that
+// miss every coupler slice (GRTF:1049-1052, 1102-1108, 1175-1178) and the R3 -> R4 switch
+// -- until the next interaction is due.  Returns that interaction's block index, or kDie
+// when the ray terminated (left eff_reg1 at GRTF:906, R5 miss at GRTF:1244-1246, or
+// range(1e5) exhausted).  Each iteration counts one bounce.
+__device__ __forceinline__ int advance(const TraceArgs &A, Lane &L, int &kind) {
+    Ray &r = L.r;
+    const double *T = L.T;
+    for (;;) {
+        if (L.bounces > (uint32_t)kMaxLoop) return kDie;
+        ++L.bounces;
+        const Cell c = locate(A.loc, r.x, r.y);
+        if (!in_poly(A.loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        const int region = r.region;
         if (region <= 1) {
-            blk = 1 + region;
             kind = 0;
-        } else if (region <= 3) {
-            const int s = first_slice(A.loc, w, kPolyFC0, nfc, r.x, r.y);
-            if (s < 0) {  // GRTF:1049-1052, 1102-1108
-                if (region == 2) {
-                    r.x += T[kTileGap + 0];
-                    r.y += T[kTileGap + 1];
-                    r.dph += 2 * T[kTileTir + 0];
-                } else if (!in_poly(A.loc, w, kPolyEff2, r.x, r.y)) {
-                    region = 4;
-                } else {
-                    r.x += T[kTileGap + 2];
-                    r.y += T[kTileGap + 3];
-                    r.dph += 2 * T[kTileTir + 1];
-                }
-                continue;
+            return 1 + region;
+        }
+        if (region <= 3) {
+            const int s = first_slice(A.loc, c, kPolyFC0, A.nfc, r.x, r.y);
+            if (s >= 0) {
+                kind = region - 1;
+                return 3 + (region - 2) * A.nfc + s;
             }
-            blk = 3 + (region - 2) * nfc + s;
-            kind = region - 1;
-        } else {
-            const int s = first_slice(A.loc, w, kPolyFC0 + nfc, noc, r.x, r.y);
-            if (s < 0) {  // GRTF:1175-1178, 1244-1246
-                if (region == 5) break;
+            if (region == 2) {
+                r.x += T[kTileGap + 0];
+                r.y += T[kTileGap + 1];
+                r.dph += 2 * T[kTileTir + 0];
+            } else if (!in_poly(A.loc, c, kPolyEff2, r.x, r.y)) {
+                r.region = 4;
+            } else {
                 r.x += T[kTileGap + 2];
                 r.y += T[kTileGap + 3];
                 r.dph += 2 * T[kTileTir + 1];
-                continue;
             }
-            blk = 3 + 2 * nfc + (region - 4) * noc + s;
-            kind = region - 1;
+            continue;
         }
-        region = interact(A, r, T, blocks + kBlock * blk, kind, false, gid, l, m, n, hit);
+        const int s = first_slice(A.loc, c, kPolyFC0 + A.nfc, A.noc, r.x, r.y);
+        if (s >= 0) {
+            kind = region - 1;
+            return 3 + 2 * A.nfc + (region - 4) * A.noc + s;
+        }
+        if (region == 5) return kDie;
+        r.x += T[kTileGap + 2];
+        r.y += T[kTileGap + 3];
+        r.dph += 2 * T[kTileTir + 1];
     }
-    A.rng[i] = r.s;
-    out.bounces = bounces;
-    out.eb_hit = hit;
-    return out;
+}
+
+__device__ __forceinline__ void lane_retire(const TraceArgs &A, const Lane &L) {
+    A.rng[L.i] = L.r.s;
+    if (A.per_ray) A.per_ray[L.i] = L.bounces;
 }
 
 __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
@@ -323,13 +375,107 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t b = 0, h = 0, bad = 0;
     if (i < A.n_rays) {
-        const RayOutcome o = trace_one(A, i);
-        b = o.bounces;
-        h = o.eb_hit;
-        bad = o.bad;
-        if (A.per_ray) A.per_ray[i] = o.bounces;
+        Lane L;
+        if (lane_load(A, i, L)) {
+            int blk = 0, kind = 0;
+            bool entry = true;
+            for (;;) {
+                const int next = interact(A, L, blk, kind, entry);
+                if (next < 0) break;
+                L.r.region = next;
+                entry = false;
+                blk = advance(A, L, kind);
+                if (blk < 0) break;
+            }
+            lane_retire(A, L);
+            b = L.bounces;
+            h = L.hit;
+        } else {
+            bad = 1;
+        }
     }
     add_stats(A.stats, b, h, bad);
+}
+
+// Variant 2: persistent waves with lane refill ("wavefront compaction" of terminated
+// rays).  Ray lifetimes are heavy-tailed (most rays die at the in-coupler, a few bounce
+// for tens of iterations), so a wave that owns 64 fixed rays idles most lanes for most of
+// its life.  Each pass of the wave loop (1) runs every live lane through its non-interacting
+// hops up to its next coupler interaction, (2) hands lanes without a ray the next rays of
+// the wave's chunk (ballot + prefix count, no memory traffic), grabbing a new chunk of
+// `chunk` consecutive rays from the global counter when the chunk runs dry, and (3) runs
+// the fp64 interaction math for all lanes together.  Results are identical to variant 1:
+// each ray's evolution depends only on its own state and its global index.
+template <int kMinWaves>
+__global__ __launch_bounds__(256, kMinWaves) void trace_persistent_kernel(TraceArgs A,
+                                                                          unsigned long long *counter,
+                                                                          int chunk) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    int64_t cur = 0, end = 0;  // wave-uniform chunk cursor
+    bool exhausted = false;
+    bool active = false;
+    Lane L;
+    int blk = 0, kind = 0;
+    bool entry = false;
+    uint64_t tot_b = 0, tot_h = 0, tot_bad = 0;
+    for (;;) {
+        if (active) {
+            blk = advance(A, L, kind);
+            entry = false;
+            if (blk < 0) {
+                lane_retire(A, L);
+                tot_b += L.bounces;
+                tot_h += L.hit;
+                active = false;
+            }
+        }
+        uint64_t need = __ballot(!active);
+        while (need != 0ull && !exhausted) {
+            if (cur >= end) {
+                unsigned long long base = 0;
+                if (lane == 0) base = atomicAdd(counter, (unsigned long long)chunk);
+                base = __shfl(base, 0);
+                if ((int64_t)base >= A.n_rays) {
+                    exhausted = true;
+                    break;
+                }
+                cur = (int64_t)base;
+                end = cur + chunk < A.n_rays ? cur + chunk : A.n_rays;
+            }
+            const int want = __popcll(need);
+            const int64_t avail = end - cur;
+            const int take = (int64_t)want < avail ? want : (int)avail;
+            if (!active) {
+                const int rank = __popcll(need & lt_mask);
+                if (rank < take) {
+                    if (lane_load(A, cur + rank, L)) {
+                        active = true;
+                        blk = 0;
+                        kind = 0;
+                        entry = true;
+                    } else {
+                        ++tot_bad;
+                    }
+                }
+            }
+            cur += take;
+            need = __ballot(!active);
+        }
+        if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
+        if (active) {
+            const int next = interact(A, L, blk, kind, entry);
+            if (next < 0) {
+                lane_retire(A, L);
+                tot_b += L.bounces;
+                tot_h += L.hit;
+                active = false;
+            } else {
+                L.r.region = next;
+            }
+        }
+    }
+    add_stats(A.stats, tot_b, tot_h, tot_bad);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -337,7 +483,7 @@ __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, con
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
     const double x = xy[2 * i], y = xy[2 * i + 1];
-    const uint64_t w = cell_word(L, x, y);
+    const Cell w = locate(L, x, y);
     uint64_t mask = 0;
     for (int k = 0; k < npoly; ++k)
         if (in_poly(L, w, k, x, y)) mask |= 1ull << k;
@@ -370,8 +516,16 @@ struct wgrt_scene {
     uint64_t *d_cells = nullptr;
     double *d_verts = nullptr;
     int32_t *d_poly_off = nullptr;
+    int32_t *d_row_off = nullptr;
+    int32_t *d_row_edges = nullptr;
     LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
     int64_t tiles = 0;
+    // work counters of the persistent kernel: a ring, so launches in flight on different
+    // streams never share one (each launch zeroes its slot with hipMemsetAsync first)
+    static constexpr int kCounterSlots = 64;
+    unsigned long long *d_counters = nullptr;
+    std::atomic<unsigned> next_counter{0};
+    int persistent_grid[2] = {0, 0};   // resident 256-thread workgroups (3 / 4 waves per SIMD)
 };
 
 namespace {
@@ -381,6 +535,8 @@ Locator make_locator(const wgrt_scene *s) {
     L.cells = s->d_cells;
     L.verts = s->d_verts;
     L.poly_off = s->d_poly_off;
+    L.row_off = s->d_row_off;
+    L.row_edges = s->d_row_edges;
     L.x0 = s->loc_host.x0;
     L.y0 = s->loc_host.y0;
     L.inv_h = s->loc_host.inv_h;
@@ -408,7 +564,7 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     *out = nullptr;
     SceneHost host;
     try {
-        build_scene_host(*desc, 0.25, host);
+        build_scene_host(*desc, 0.125, host);
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
@@ -427,13 +583,30 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     wgrt_status st;
     if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK ||
         (st = upload(host.loc.verts, &s->d_verts)) != WGRT_OK ||
-        (st = upload(host.loc.poly_off, &s->d_poly_off)) != WGRT_OK) {
+        (st = upload(host.loc.poly_off, &s->d_poly_off)) != WGRT_OK ||
+        (st = upload(host.loc.row_off, &s->d_row_off)) != WGRT_OK ||
+        (st = upload(host.loc.row_edges, &s->d_row_edges)) != WGRT_OK) {
         wgrt_scene_destroy(s);
         return st;
+    }
+    {
+        hipError_t e = hipMalloc((void **)&s->d_counters, sizeof(unsigned long long) * wgrt_scene::kCounterSlots);
+        if (e != hipSuccess) {
+            wgrt_scene_destroy(s);
+            return fail(WGRT_ERR_HIP, std::string("hipMalloc(counters): ") + hipGetErrorString(e));
+        }
+        int cus = 0, per_cu3 = 0, per_cu4 = 0;
+        HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, trace_persistent_kernel<3>, 256, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, trace_persistent_kernel<4>, 256, 0));
+        s->persistent_grid[0] = std::max(1, cus * std::max(1, per_cu3));
+        s->persistent_grid[1] = std::max(1, cus * std::max(1, per_cu4));
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
     s->loc_host.cells.shrink_to_fit();
+    s->loc_host.row_edges.clear();
+    s->loc_host.row_edges.shrink_to_fit();
     *out = s;
     return WGRT_OK;
 }
@@ -445,6 +618,9 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     hipFree(s->d_cells);
     hipFree(s->d_verts);
     hipFree(s->d_poly_off);
+    hipFree(s->d_counters);
+    hipFree(s->d_row_off);
+    hipFree(s->d_row_edges);
     delete s;
     return WGRT_OK;
 }
@@ -472,8 +648,7 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
     if (!rays->x || !rays->y || !rays->m || !rays->n || !rays->lmd_num || !rays->te || !rays->tm ||
         !rays->delta_phase || !rng_states || !matrix_EB)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL ray column / rng_states / matrix_EB");
-    if (variant < 0 || variant > 2) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
-    (void)workgroups;
+    if (variant < 0 || variant > 3) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
     TraceArgs A;
     A.x = rays->x;
     A.y = rays->y;
@@ -499,9 +674,23 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
     A.nl = s->nl;
     A.n_g = s->n_g;
     hipStream_t st = (hipStream_t)stream;
-    const int64_t blocks = (n_rays + 255) / 256;
-    if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
-    hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
+    if (variant == 1) {
+        const int64_t blocks = (n_rays + 255) / 256;
+        if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
+        hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
+    } else {
+        wgrt_scene *ms = const_cast<wgrt_scene *>(s);
+        unsigned long long *ctr = ms->d_counters + (ms->next_counter++ % wgrt_scene::kCounterSlots);
+        HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st));
+        const bool four = variant == 3;
+        int64_t grid = workgroups > 0 ? workgroups : s->persistent_grid[four ? 1 : 0];
+        const int64_t useful = (n_rays + 255) / 256;   // never more workgroups than rays / 256
+        if (grid > useful) grid = useful;
+        if (four)
+            hipLaunchKernelGGL(trace_persistent_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
+        else
+            hipLaunchKernelGGL(trace_persistent_kernel<3>, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
+    }
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }

@@ -122,7 +122,8 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
 
 /* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
  * count for the persistent variant (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
- * grid, 2 persistent wave-refill. */
+ * grid, 2 persistent wave-refill (3 waves / SIMD), 3 persistent wave-refill built for
+ * 4 waves / SIMD (register spills).  All variants produce identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,

@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Interleaved A/B timing of kernel variants in ONE process (methodology rule 24).
+
+Builds the C3 workload once, checks every variant's outputs are identical after one
+launch from the same state, then times rounds x variants interleaved and prints the
+median / min kernel time and bounces/s per variant as one JSON line each.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--variants", default="1,2")
+    ap.add_argument("--workgroups", default="0", help="comma list matching --variants (0 = auto)")
+    ap.add_argument("--rounds", type=int, default=10)
+    ap.add_argument("--nx", type=int, default=21)
+    ap.add_argument("--ny", type=int, default=21)
+    ap.add_argument("--R", type=int, default=1024)
+    ap.add_argument("--profile", default="default")
+    a = ap.parse_args()
+    import torch
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, rays_to_device, trace_fullcolor
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, generate_points_in_polygon, rng_seeds
+
+    dev = torch.device("cuda", 0)
+    geom = design_geometry(a.nx, a.ny)
+    luts = synthetic_luts(geom, seed=0, profile=a.profile)
+    pts = generate_points_in_polygon(geom.IC, a.R // 2, rng=np.random.default_rng(1))
+    host = build_rays(pts, a.nx, a.ny, [0, 1, 2], a.R)
+    N = host["x"].shape[0]
+    scene = Scene.from_geometry(geom, luts)
+    rays = rays_to_device(host, dev)
+    seeds = torch.from_numpy(rng_seeds(N).view(np.int32)).to(dev)
+    variants = [int(v) for v in a.variants.split(",")]
+    wgs = [int(w) for w in a.workgroups.split(",")]
+    wgs = wgs + [wgs[-1]] * (len(variants) - len(wgs))
+
+    ref = None
+    for v, wg in zip(variants, wgs):
+        rng = seeds.clone()
+        eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+        st = torch.zeros(4, dtype=torch.int64, device=dev)
+        trace_fullcolor(scene, rays, rng, eb, stats=st, variant=v, workgroups=wg)
+        torch.cuda.synchronize()
+        out = (rng.cpu(), eb.cpu(), st.cpu())
+        if ref is None:
+            ref = out
+        else:
+            same = torch.equal(out[0], ref[0]) and torch.equal(out[1], ref[1]) and torch.equal(out[2], ref[2])
+            print(json.dumps({"variant": v, "identical_to_first": bool(same)}))
+    bounces = int(ref[2][0])
+    times = {k: [] for k in range(len(variants))}
+    rng = seeds.clone()
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    for _ in range(a.rounds):
+        for k, (v, wg) in enumerate(zip(variants, wgs)):
+            rng.copy_(seeds)
+            s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s.record()
+            trace_fullcolor(scene, rays, rng, eb, variant=v, workgroups=wg)
+            e.record()
+            torch.cuda.synchronize()
+            times[k].append(s.elapsed_time(e))
+    for k, (v, wg) in enumerate(zip(variants, wgs)):
+        t = np.array(times[k])
+        print(json.dumps({"variant": v, "workgroups": wg, "median_ms": round(float(np.median(t)), 4),
+                          "min_ms": round(float(t.min()), 4), "bounces": bounces,
+                          "bounces_per_s": round(bounces / (np.median(t) / 1e3), 1), "rays": N}))
+
+
+if __name__ == "__main__":
+    main()
