@@ -61,7 +61,8 @@ class SceneInfo(ctypes.Structure):
     _fields_ = [("tile_bytes", ctypes.c_int64), ("tiles", ctypes.c_int64),
                 ("grid_cells_x", ctypes.c_int64), ("grid_cells_y", ctypes.c_int64),
                 ("grid_cell_mm", ctypes.c_double), ("grid_edge_cells", ctypes.c_int64),
-                ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32)]
+                ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32),
+                ("lds_locator_bytes", ctypes.c_int64), ("lds_cell_mm", ctypes.c_double)]
 
 
 _lib = None

@@ -25,6 +25,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <atomic>
 #include <mutex>
@@ -40,6 +41,14 @@ using namespace wgrt;
 namespace {
 
 thread_local std::string g_last_error;
+// Miss hops a lane may take per pass of the persistent loop before the wave's interaction
+// step (env WGRT_MAX_HOPS, 0 = unbounded).  Bounding it keeps lanes whose ray is crossing a
+// coupler-free stretch from stalling the whole wave; 2 measured best on the C3 workload
+// (0.92 ms vs 1.05 ms unbounded, tools/ab.py).  Scheduling only: results are identical.
+int g_max_hops = [] {
+    const char *v = getenv("WGRT_MAX_HOPS");
+    return v ? atoi(v) : 2;
+}();
 
 wgrt_status fail(wgrt_status s, const std::string &msg) {
     g_last_error = msg;
@@ -56,12 +65,26 @@ wgrt_status fail(wgrt_status s, const std::string &msg) {
 // ----------------------------------------------------------------------------
 // device-side scene view
 // ----------------------------------------------------------------------------
-struct Locator {
-    const uint64_t *cells;
+// The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t for the global-memory
+// copy (up to 32 polygons), uint32_t for the LDS-resident copy (up to 16 polygons).
+template <class CellT>
+struct LocatorT {
+    const CellT *cells;
     const double *verts;
     const int32_t *poly_off;
     const int32_t *row_off;
     const int32_t *row_edges;
+    double x0, y0, inv_h;
+    int ncx, ncy;
+};
+using Locator = LocatorT<uint64_t>;
+
+// Where the LDS-resident locator lives inside the dynamic LDS of the persistent kernel, and
+// where its source copy lives in global memory (all byte offsets are multiples of 16).
+struct LdsLocatorDesc {
+    const char *src;         // global image, copied verbatim into LDS at kernel start
+    int bytes;               // image size
+    int off_cells, off_verts, off_poly, off_row_off, off_row_edges;
     double x0, y0, inv_h;
     int ncx, ncy;
 };
@@ -75,8 +98,10 @@ struct TraceArgs {
     int64_t n_rays, gid_offset;
     const double *tiles;
     Locator loc;
+    LdsLocatorDesc lds;
     int tile_d, nfc, noc, nx, ny, nl;
-    double n_g;
+    double n_g, inv_n_g;
+    int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
 };
 
 constexpr int kPolyEff1 = 0;
@@ -90,18 +115,20 @@ struct Cell {
     int cy;
 };
 
-__device__ __forceinline__ Cell locate(const Locator &L, double x, double y) {
+template <class Loc>
+__device__ __forceinline__ Cell locate(const Loc &L, double x, double y) {
     const double fx = floor((x - L.x0) * L.inv_h);
     const double fy = floor((y - L.y0) * L.inv_h);
     // NaN / out-of-grid points are outside every polygon (cell word 0 = all OUT)
     if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return Cell{0ull, 0};
     const int cx = (int)fx, cy = (int)fy;
-    return Cell{L.cells[cy * L.ncx + cx], cy};
+    return Cell{(uint64_t)L.cells[cy * L.ncx + cx], cy};
 }
 
 // is_inside_or_on_edge(x, y, polygon k) (GRTF:63-71): the cell class when the cell is IN or
 // OUT, else the reference predicate over the polygon's edges that meet the cell's row.
-__device__ __forceinline__ bool in_poly(const Locator &L, const Cell &c, int k, double x, double y) {
+template <class Loc>
+__device__ __forceinline__ bool in_poly(const Loc &L, const Cell &c, int k, double x, double y) {
     const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
     const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
@@ -114,7 +141,8 @@ __device__ __forceinline__ bool in_poly(const Locator &L, const Cell &c, int k, 
 // -1 if none (the slice scans of GRTF:1002-1005 and GRTF:1112-1115, which stop at the
 // first hit).  Candidates come straight from the cell word: a slice is tested exactly only
 // when its class is EDGE; an IN slice is a hit; OUT slices are skipped.
-__device__ __forceinline__ int first_slice(const Locator &L, const Cell &c, int first, int count,
+template <class Loc>
+__device__ __forceinline__ int first_slice(const Loc &L, const Cell &c, int first, int count,
                                            double x, double y) {
     uint64_t f = c.w >> (2 * first);
     if (count < 32) f &= (1ull << (2 * count)) - 1ull;
@@ -196,53 +224,97 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
     return true;
 }
 
-enum : int { kDie = -1 };
+enum : int { kDie = -1, kTransit = -2 };
+
+#ifdef WGRT_DIAG
+// Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
+__device__ unsigned long long g_diag[16];
+__device__ unsigned long long g_diag_fallback;
+#endif
 
 // A coupler interaction: `blk` of the lane's tile, `kind` 0 in-coupler states (entry event,
 // R0, R1), 1 R2, 2 R3, 3 R4, 4 R5.  Evaluates every branch's efficiency (GRTF:860-869,
 // 909-918, ..., 1186-1200), draws, and applies the chosen branch.  Returns the next region
 // or kDie.  Only the chosen branch's phase (two atan2) is evaluated; its field is recomputed
 // by the same operations rather than kept in registers for every branch.
-__device__ __forceinline__ int interact(const TraceArgs &A, Lane &L, int blk, int kind, bool entry) {
+template <class Loc>
+__device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane &L, int blk, int kind,
+                                        bool entry) {
     Ray &r = L.r;
     const double *T = L.T;
     const double *B = T + kTileHeader + kBlock * blk;
     double sd, cd;
     sincos(r.dph, &sd, &cd);
     const bool three = kind >= 3;
-    const double denom = entry ? T[kTileCosIc1] : r.cos_t;
-    double te[3], tm[3];
-    {
-        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec);
-        te[0] = hypot_cr(f.te_re, f.te_im);
-        tm[0] = hypot_cr(f.tm_re, f.tm_im);
-    }
-    {
-        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8);
-        te[1] = hypot_cr(f.te_re, f.te_im);
-        tm[1] = hypot_cr(f.tm_re, f.tm_im);
-    }
-    te[2] = tm[2] = 0.0;
-    if (three) {
-        const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 16);
-        te[2] = hypot_cr(f.te_re, f.te_im);
-        tm[2] = hypot_cr(f.tm_re, f.tm_im);
-    }
-    double e0 = (te[0] * te[0] + tm[0] * tm[0]) * B[0] / denom;
-    double e1 = (te[1] * te[1] + tm[1] * tm[1]) * B[1] / denom;
-    if (entry) {
-        e0 = e0 * A.n_g;
-        e1 = e1 * A.n_g;
-    }
-    double e2 = 0.0;
-    if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
-    const double u = rng_draw(r.s, A.gid_offset + L.i);
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
+    const double denom = entry ? T[kTileCosIc1] : r.cos_t;
+    const double u = rng_draw(r.s, A.gid_offset + L.i);
+
+    // Decide the branch.  The reference compares u with cumulative branch efficiencies
+    // e_k = (hypot(Ete')^2 + hypot(Etm')^2) * cosA_k / cos(theta) [* or / n_g].  Here the
+    // comparisons are first made with cheap estimates (squared moduli instead of the
+    // correctly rounded hypot, one reciprocal instead of three divisions), whose relative
+    // error is below 1e-14; a decision is accepted only when every threshold it depends on
+    // is farther than 1e-12 (relative) from u and no product can underflow, which makes it
+    // provably the reference's decision.  Otherwise -- about once in 1e12 draws -- the lane
+    // recomputes every e_k exactly as the reference does.  The chosen branch's magnitudes
+    // and efficiency are always computed exactly.
+    double q[3];
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        q[k] = 0.0;
+        if (k < 2 || three) {
+            const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
+            q[k] = (f.te_re * f.te_re + f.te_im * f.te_im) + (f.tm_re * f.tm_re + f.tm_im * f.tm_im);
+        }
+    }
+    const double inv = 1.0 / denom;
+    double a0 = q[0] * B[0] * inv, a1 = q[1] * B[1] * inv;
+    if (entry) {
+        a0 *= A.n_g;
+        a1 *= A.n_g;
+    }
+    const double a2 = three ? q[2] * B[2] * inv * A.inv_n_g : 0.0;
+    const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
+    const double scale = fabs(a0) + fabs(a1) + fabs(a2);   // bounds every partial sum
+    const double tol = 1e-12 * scale;
+    const bool tiny = thr && !(r.ener > 1e-200 && (a0 == 0.0 || a0 > 1e-100) && (a1 == 0.0 || a1 > 1e-100) &&
+                               (!three || a2 == 0.0 || a2 > 1e-100));
+    const bool sure = scale > 1e-290 && !tiny && fabs(u - c0) > tol && fabs(u - c1) > tol &&
+                      (!three || fabs(u - c2) > tol);
     int b;
-    if (u <= e0 && (!thr || r.ener * e0 > 0.0)) b = 0;
-    else if (u <= e0 + e1 && (!thr || r.ener * e1 > 0.0)) b = 1;
-    else if (three && u <= e0 + e1 + e2 && r.ener * e2 > 0.0) b = 2;
-    else return kDie;
+    if (sure) {
+        if (u <= c0 && (!thr || a0 > 0.0)) b = 0;
+        else if (u <= c1 && (!thr || a1 > 0.0)) b = 1;
+        else if (three && u <= c2 && a2 > 0.0) b = 2;
+        else return kDie;
+    } else {
+#ifdef WGRT_DIAG
+        atomicAdd(&g_diag_fallback, 1ull);
+#endif
+        double te[3], tm[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            te[k] = tm[k] = 0.0;
+            if (k < 2 || three) {
+                const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
+                te[k] = hypot_cr(f.te_re, f.te_im);
+                tm[k] = hypot_cr(f.tm_re, f.tm_im);
+            }
+        }
+        double e0 = (te[0] * te[0] + tm[0] * tm[0]) * B[0] / denom;
+        double e1 = (te[1] * te[1] + tm[1] * tm[1]) * B[1] / denom;
+        if (entry) {
+            e0 = e0 * A.n_g;
+            e1 = e1 * A.n_g;
+        }
+        double e2 = 0.0;
+        if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
+        if (u <= e0 && (!thr || r.ener * e0 > 0.0)) b = 0;
+        else if (u <= e0 + e1 && (!thr || r.ener * e1 > 0.0)) b = 1;
+        else if (three && u <= e0 + e1 + e2 && r.ener * e2 > 0.0) b = 2;
+        else return kDie;
+    }
 
     if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
         if (inside_or_on_edge(r.x, r.y, T + kTileEbRect, 4)) {
@@ -264,10 +336,11 @@ __device__ __forceinline__ int interact(const TraceArgs &A, Lane &L, int blk, in
         }
         return kDie;
     }
-    const double cte = b == 0 ? te[0] : te[1];
-    const double ctm = b == 0 ? tm[0] : tm[1];
-    const double e = b == 0 ? e0 : e1;
     const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * b);
+    const double cte = hypot_cr(f.te_re, f.te_im);
+    const double ctm = hypot_cr(f.tm_re, f.tm_im);
+    double e = (cte * cte + ctm * ctm) * B[b] / denom;   // exact e_b (GRTF:868-869, 917-918, ...)
+    if (entry) e = e * A.n_g;
     // take the branch (GRTF:872-882 and every branch body after it)
     const double norm = sqrt(cte * cte + ctm * ctm);
     const double ph = efield_phase(f, cte, ctm);
@@ -283,7 +356,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, Lane &L, int blk, in
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
     if (kind == 0) {
-        const bool in_ic = in_poly(A.loc, locate(A.loc, r.x, r.y), kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly(loc, locate(loc, r.x, r.y), kPolyIC, r.x, r.y);
         if (b == 0) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -296,47 +369,48 @@ __device__ __forceinline__ int interact(const TraceArgs &A, Lane &L, int blk, in
 // -- until the next interaction is due.  Returns that interaction's block index, or kDie
 // when the ray terminated (left eff_reg1 at GRTF:906, R5 miss at GRTF:1244-1246, or
 // range(1e5) exhausted).  Each iteration counts one bounce.
-__device__ __forceinline__ int advance(const TraceArgs &A, Lane &L, int &kind) {
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane &L, int &kind) {
     Ray &r = L.r;
     const double *T = L.T;
-    for (;;) {
+    // A miss hop's step is fixed by the region: R2 moves by gap[0:2] and adds 2*TIR[0],
+    // R3 and R4 move by gap[2:4] and add 2*TIR[1] (R5 misses die).  Fetch it once.
+    const int g = (r.region == 2) ? 0 : 2;
+    const double gx = T[kTileGap + g], gy = T[kTileGap + g + 1];
+    const double dtir = 2 * T[kTileTir + (g >> 1)];
+    for (int hops = 0;; ++hops) {
+        if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
-        const Cell c = locate(A.loc, r.x, r.y);
-        if (!in_poly(A.loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        const Cell c = locate(loc, r.x, r.y);
+        if (!in_poly(loc, c, kPolyEff1, r.x, r.y)) return kDie;
         const int region = r.region;
         if (region <= 1) {
             kind = 0;
             return 1 + region;
         }
+        int s;
         if (region <= 3) {
-            const int s = first_slice(A.loc, c, kPolyFC0, A.nfc, r.x, r.y);
+            s = first_slice(loc, c, kPolyFC0, A.nfc, r.x, r.y);
             if (s >= 0) {
                 kind = region - 1;
                 return 3 + (region - 2) * A.nfc + s;
             }
-            if (region == 2) {
-                r.x += T[kTileGap + 0];
-                r.y += T[kTileGap + 1];
-                r.dph += 2 * T[kTileTir + 0];
-            } else if (!in_poly(A.loc, c, kPolyEff2, r.x, r.y)) {
-                r.region = 4;
-            } else {
-                r.x += T[kTileGap + 2];
-                r.y += T[kTileGap + 3];
-                r.dph += 2 * T[kTileTir + 1];
+            if (region == 3 && !in_poly(loc, c, kPolyEff2, r.x, r.y)) {
+                r.region = 4;   // GRTF:1103-1104: switch to the out-coupler state without moving
+                continue;
             }
-            continue;
+        } else {
+            s = first_slice(loc, c, kPolyFC0 + A.nfc, A.noc, r.x, r.y);
+            if (s >= 0) {
+                kind = region - 1;
+                return 3 + 2 * A.nfc + (region - 4) * A.noc + s;
+            }
+            if (region == 5) return kDie;
         }
-        const int s = first_slice(A.loc, c, kPolyFC0 + A.nfc, A.noc, r.x, r.y);
-        if (s >= 0) {
-            kind = region - 1;
-            return 3 + 2 * A.nfc + (region - 4) * A.noc + s;
-        }
-        if (region == 5) return kDie;
-        r.x += T[kTileGap + 2];
-        r.y += T[kTileGap + 3];
-        r.dph += 2 * T[kTileTir + 1];
+        r.x += gx;
+        r.y += gy;
+        r.dph += dtir;
     }
 }
 
@@ -350,23 +424,16 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
     return v;
 }
 
-__device__ void add_stats(wgrt_trace_stats *stats, uint64_t bounces, uint64_t hits, uint64_t bad) {
-    __shared__ unsigned long long red[3];
-    if (threadIdx.x == 0) red[0] = red[1] = red[2] = 0ull;
-    __syncthreads();
+// Per-wave reduction of the ray counters, then one 64-bit atomic per counter per wave.
+__device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t bounces, uint64_t hits,
+                                          uint64_t bad) {
     bounces = wave_sum(bounces);
     hits = wave_sum(hits);
     bad = wave_sum(bad);
-    if ((threadIdx.x & 63) == 0) {
-        atomicAdd(&red[0], (unsigned long long)bounces);
-        atomicAdd(&red[1], (unsigned long long)hits);
-        atomicAdd(&red[2], (unsigned long long)bad);
-    }
-    __syncthreads();
-    if (threadIdx.x == 0 && stats) {
-        atomicAdd((unsigned long long *)&stats->bounces, red[0]);
-        atomicAdd((unsigned long long *)&stats->eyebox_hits, red[1]);
-        atomicAdd((unsigned long long *)&stats->bad_rays, red[2]);
+    if ((threadIdx.x & 63) == 0 && stats) {
+        if (bounces) atomicAdd((unsigned long long *)&stats->bounces, (unsigned long long)bounces);
+        if (hits) atomicAdd((unsigned long long *)&stats->eyebox_hits, (unsigned long long)hits);
+        if (bad) atomicAdd((unsigned long long *)&stats->bad_rays, (unsigned long long)bad);
     }
 }
 
@@ -380,11 +447,13 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
             int blk = 0, kind = 0;
             bool entry = true;
             for (;;) {
-                const int next = interact(A, L, blk, kind, entry);
+                const int next = interact(A, A.loc, L, blk, kind, entry);
                 if (next < 0) break;
                 L.r.region = next;
                 entry = false;
-                blk = advance(A, L, kind);
+                do {
+                    blk = advance(A, A.loc, L, kind);
+                } while (blk == kTransit);
                 if (blk < 0) break;
             }
             lane_retire(A, L);
@@ -406,10 +475,9 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 // `chunk` consecutive rays from the global counter when the chunk runs dry, and (3) runs
 // the fp64 interaction math for all lanes together.  Results are identical to variant 1:
 // each ray's evolution depends only on its own state and its global index.
-template <int kMinWaves>
-__global__ __launch_bounds__(256, kMinWaves) void trace_persistent_kernel(TraceArgs A,
-                                                                          unsigned long long *counter,
-                                                                          int chunk) {
+template <class Loc>
+__device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &loc, unsigned long long *counter,
+                                                int chunk) {
     const int lane = threadIdx.x & 63;
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int64_t cur = 0, end = 0;  // wave-uniform chunk cursor
@@ -419,11 +487,23 @@ __global__ __launch_bounds__(256, kMinWaves) void trace_persistent_kernel(TraceA
     int blk = 0, kind = 0;
     bool entry = false;
     uint64_t tot_b = 0, tot_h = 0, tot_bad = 0;
+#ifdef WGRT_DIAG
+    uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_hopmax = 0;
+#endif
     for (;;) {
         if (active) {
-            blk = advance(A, L, kind);
+#ifdef WGRT_DIAG
+            const uint32_t b0 = L.bounces;
+#endif
+            blk = advance(A, loc, L, kind);
+#ifdef WGRT_DIAG
+            uint32_t hops = L.bounces - b0 - (blk >= 0 ? 1u : 0u);
+            d_hops += hops;
+            for (int o = 32; o > 0; o >>= 1) hops = max(hops, (uint32_t)__shfl_xor((int)hops, o));
+            d_hopmax += hops;
+#endif
             entry = false;
-            if (blk < 0) {
+            if (blk == kDie) {
                 lane_retire(A, L);
                 tot_b += L.bounces;
                 tot_h += L.hit;
@@ -463,8 +543,19 @@ __global__ __launch_bounds__(256, kMinWaves) void trace_persistent_kernel(TraceA
             need = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
-        if (active) {
-            const int next = interact(A, L, blk, kind, entry);
+#ifdef WGRT_DIAG
+        {
+            const uint64_t na = __popcll(__ballot(active));
+            d_pass += 1;
+            d_act += na;
+            if (exhausted) {
+                d_pass_x += 1;
+                d_act_x += na;
+            }
+        }
+#endif
+        if (active && blk >= 0) {
+            const int next = interact(A, loc, L, blk, kind, entry);
             if (next < 0) {
                 lane_retire(A, L);
                 tot_b += L.bounces;
@@ -476,6 +567,51 @@ __global__ __launch_bounds__(256, kMinWaves) void trace_persistent_kernel(TraceA
         }
     }
     add_stats(A.stats, tot_b, tot_h, tot_bad);
+#ifdef WGRT_DIAG
+    if (lane == 0) {
+        atomicAdd(&g_diag[0], d_pass);
+        atomicAdd(&g_diag[1], d_act);
+        atomicAdd(&g_diag[2], d_pass_x);
+        atomicAdd(&g_diag[3], d_act_x);
+        atomicAdd(&g_diag[5], d_hopmax);
+    }
+    d_hops = wave_sum(d_hops);
+    if (lane == 0) atomicAdd(&g_diag[4], d_hops);
+#endif
+}
+
+// Variant 2: the persistent loop with the locator read from global memory (L2-resident).
+__global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, unsigned long long *counter,
+                                                                  int chunk) {
+    persistent_body(A, A.loc, counter, chunk);
+}
+
+// Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
+// row-band edge lists) staged once into LDS by every workgroup, so the per-hop membership
+// tests cost LDS reads instead of dependent L2 round trips.  One 768-thread workgroup
+// (12 waves, 3 per SIMD) per CU shares one LDS copy of up to ~150 KB.
+__global__ __launch_bounds__(768, 1) void trace_persistent_lds_kernel(TraceArgs A, unsigned long long *counter,
+                                                                      int chunk) {
+    extern __shared__ __attribute__((aligned(16))) char smem[];
+    const LdsLocatorDesc &D = A.lds;
+    {
+        const uint4 *src = (const uint4 *)D.src;
+        uint4 *dst = (uint4 *)smem;
+        for (int k = threadIdx.x; k < D.bytes / 16; k += blockDim.x) dst[k] = src[k];
+    }
+    __syncthreads();
+    LocatorT<uint32_t> loc;
+    loc.cells = (const uint32_t *)(smem + D.off_cells);
+    loc.verts = (const double *)(smem + D.off_verts);
+    loc.poly_off = (const int32_t *)(smem + D.off_poly);
+    loc.row_off = (const int32_t *)(smem + D.off_row_off);
+    loc.row_edges = (const int32_t *)(smem + D.off_row_edges);
+    loc.x0 = D.x0;
+    loc.y0 = D.y0;
+    loc.inv_h = D.inv_h;
+    loc.ncx = D.ncx;
+    loc.ncy = D.ncy;
+    persistent_body(A, loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -525,7 +661,11 @@ struct wgrt_scene {
     static constexpr int kCounterSlots = 64;
     unsigned long long *d_counters = nullptr;
     std::atomic<unsigned> next_counter{0};
-    int persistent_grid[2] = {0, 0};   // resident 256-thread workgroups (3 / 4 waves per SIMD)
+    int persistent_grid = 0;   // resident 256-thread workgroups of variant 2
+    int lds_grid = 0;          // resident 768-thread workgroups of variant 3 (0: unavailable)
+    char *d_lds_image = nullptr;
+    size_t lds_bytes = 0;
+    LdsImage lds;              // offsets / grid parameters (bytes released after upload)
 };
 
 namespace {
@@ -595,12 +735,35 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
             wgrt_scene_destroy(s);
             return fail(WGRT_ERR_HIP, std::string("hipMalloc(counters): ") + hipGetErrorString(e));
         }
-        int cus = 0, per_cu3 = 0, per_cu4 = 0;
+        int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu3, trace_persistent_kernel<3>, 256, 0));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu4, trace_persistent_kernel<4>, 256, 0));
-        s->persistent_grid[0] = std::max(1, cus * std::max(1, per_cu3));
-        s->persistent_grid[1] = std::max(1, cus * std::max(1, per_cu4));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_kernel, 256, 0));
+        s->persistent_grid = std::max(1, cus * std::max(1, per_cu));
+        if (host.lds.ok) {
+            const int bytes = (int)host.lds.bytes.size();
+            int lds_max = 0;
+            HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
+            if (bytes <= lds_max) {
+                (void)hipFuncSetAttribute((const void *)trace_persistent_lds_kernel,
+                                          hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
+                int per_cu_lds = 0;
+                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_lds, trace_persistent_lds_kernel,
+                                                                     768, bytes));
+                if (per_cu_lds > 0) {
+                    wgrt_status st2 = upload(host.lds.bytes, &s->d_lds_image);
+                    if (st2 != WGRT_OK) {
+                        wgrt_scene_destroy(s);
+                        return st2;
+                    }
+                    s->lds_grid = cus * per_cu_lds;
+                }
+            }
+        }
+        s->lds_bytes = host.lds.bytes.size();
+        s->lds = host.lds;
+        s->lds.bytes.clear();
+        s->lds.bytes.shrink_to_fit();
+        s->lds.ok = s->lds_grid > 0;
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
@@ -613,14 +776,15 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
 
 wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     if (!s) return WGRT_OK;
-    hipSetDevice(s->device);
-    hipFree(s->d_tiles);
-    hipFree(s->d_cells);
-    hipFree(s->d_verts);
-    hipFree(s->d_poly_off);
-    hipFree(s->d_counters);
-    hipFree(s->d_row_off);
-    hipFree(s->d_row_edges);
+    (void)hipSetDevice(s->device);
+    (void)hipFree(s->d_tiles);
+    (void)hipFree(s->d_cells);
+    (void)hipFree(s->d_verts);
+    (void)hipFree(s->d_poly_off);
+    (void)hipFree(s->d_counters);
+    (void)hipFree(s->d_row_off);
+    (void)hipFree(s->d_row_edges);
+    (void)hipFree(s->d_lds_image);
     delete s;
     return WGRT_OK;
 }
@@ -634,6 +798,8 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->grid_cell_mm = s->loc_host.h;
     info->grid_edge_cells = s->loc_host.edge_cells;
     info->n_polygons = s->npoly;
+    info->lds_locator_bytes = s->lds_grid > 0 ? (int64_t)s->lds_bytes : 0;
+    info->lds_cell_mm = s->lds_grid > 0 ? s->lds.h : 0.0;
     info->device = s->device;
     return WGRT_OK;
 }
@@ -666,6 +832,7 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
     A.gid_offset = gid_offset;
     A.tiles = s->d_tiles;
     A.loc = make_locator(s);
+    A.lds = LdsLocatorDesc{};
     A.tile_d = s->tile_d;
     A.nfc = s->nfc;
     A.noc = s->noc;
@@ -673,23 +840,42 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
     A.ny = s->ny;
     A.nl = s->nl;
     A.n_g = s->n_g;
+    A.inv_n_g = 1.0 / s->n_g;
+    A.max_hops = g_max_hops;
     hipStream_t st = (hipStream_t)stream;
     if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
         if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
         hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
     } else {
+        const bool use_lds = variant == 3 || (variant == 0 && s->lds_grid > 0);
+        if (use_lds && s->lds_grid == 0)
+            return fail(WGRT_ERR_UNSUPPORTED, "variant 3 needs the locator to fit in LDS (<= 16 polygons)");
         wgrt_scene *ms = const_cast<wgrt_scene *>(s);
         unsigned long long *ctr = ms->d_counters + (ms->next_counter++ % wgrt_scene::kCounterSlots);
         HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st));
-        const bool four = variant == 3;
-        int64_t grid = workgroups > 0 ? workgroups : s->persistent_grid[four ? 1 : 0];
-        const int64_t useful = (n_rays + 255) / 256;   // never more workgroups than rays / 256
+        const int tpb = use_lds ? 768 : 256;
+        int64_t grid = workgroups > 0 ? workgroups : (use_lds ? s->lds_grid : s->persistent_grid);
+        const int64_t useful = (n_rays + tpb - 1) / tpb;   // never more workgroups than rays / tpb
         if (grid > useful) grid = useful;
-        if (four)
-            hipLaunchKernelGGL(trace_persistent_kernel<4>, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
-        else
-            hipLaunchKernelGGL(trace_persistent_kernel<3>, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
+        if (use_lds) {
+            A.lds.src = s->d_lds_image;
+            A.lds.bytes = (int)s->lds_bytes;
+            A.lds.off_cells = s->lds.off_cells;
+            A.lds.off_verts = s->lds.off_verts;
+            A.lds.off_poly = s->lds.off_poly;
+            A.lds.off_row_off = s->lds.off_row_off;
+            A.lds.off_row_edges = s->lds.off_row_edges;
+            A.lds.x0 = s->lds.x0;
+            A.lds.y0 = s->lds.y0;
+            A.lds.inv_h = s->lds.inv_h;
+            A.lds.ncx = s->lds.ncx;
+            A.lds.ncy = s->lds.ncy;
+            hipLaunchKernelGGL(trace_persistent_lds_kernel, dim3((unsigned)grid), dim3(768), (unsigned)s->lds_bytes,
+                               st, A, ctr, 64);
+        } else {
+            hipLaunchKernelGGL(trace_persistent_kernel, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
+        }
     }
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
@@ -737,5 +923,20 @@ const char *wgrt_status_string(wgrt_status s) {
 const char *wgrt_last_error(void) { return g_last_error.c_str(); }
 
 int wgrt_abi_version(void) { return WGRT_ABI_VERSION; }
+
+#ifdef WGRT_DIAG
+// Diagnostic build only: read-and-reset the wave-loop counters (synchronous).
+int wgrt_diag_read(unsigned long long *out17) {
+    unsigned long long h[16], fb = 0;
+    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) != hipSuccess) return 2;
+    if (hipMemcpyFromSymbol(&fb, HIP_SYMBOL(g_diag_fallback), sizeof(fb)) != hipSuccess) return 2;
+    for (int k = 0; k < 16; ++k) out17[k] = h[k];
+    out17[16] = fb;
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_fallback), z, sizeof(fb));
+    return 0;
+}
+#endif
 
 }  // extern "C"

@@ -99,6 +99,8 @@ typedef struct {
     int64_t grid_edge_cells;   /* cells whose class needs the exact polygon test      */
     int32_t n_polygons;
     int32_t device;
+    int64_t lds_locator_bytes; /* LDS image of the locator for variant 3 (0: does not fit) */
+    double lds_cell_mm;        /* its cell size                                       */
 } wgrt_scene_info;
 
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon
@@ -122,8 +124,9 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
 
 /* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
  * count for the persistent variant (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
- * grid, 2 persistent wave-refill (3 waves / SIMD), 3 persistent wave-refill built for
- * 4 waves / SIMD (register spills).  All variants produce identical results. */
+ * grid, 2 persistent wave-refill (locator in global memory), 3 persistent wave-refill with
+ * the locator staged in LDS (needs <= 16 polygons; WGRT_ERR_UNSUPPORTED otherwise).  Auto
+ * picks 3 when available, else 2.  All variants produce identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,

@@ -50,7 +50,7 @@ def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0):
 from tests._fixtures import CASES, GoldenCase  # noqa: E402
 
 
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 @pytest.mark.parametrize("name", CASES)
 def test_golden_exact(dev, name, variant):
     case = GoldenCase(name)
@@ -92,7 +92,7 @@ def _config(nx, ny, lambdas, R, seed=0, profile="default", point_seed=1):
     dict(nx=21, ny=21, lambdas=[0, 1, 2], R=256),                     # C3 grid, fewer rays
     dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="deep", seed=5),
 ])
-@pytest.mark.parametrize("variant", [1, 2])
+@pytest.mark.parametrize("variant", [1, 2, 3])
 def test_matches_oracle_at_scale(dev, cfg, variant):
     from oracle import OracleScene
     c = _config(**cfg)
