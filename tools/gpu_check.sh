@@ -1,7 +1,7 @@
 #!/bin/bash
-# One GPU session: parity tests, smoke, bench, rocprofv3 kernel-trace summary.
-# Stops at the first step that dies abnormally (fault / abort / timeout); plain test
-# failures (pytest exit 1) are recorded and the later steps still run.
+# One GPU session: parity tests, smoke, PMC traffic passes, bench, rocprofv3 kernel-trace
+# summary.  Stops at the first step that dies abnormally (fault / abort / timeout); plain
+# test failures (pytest exit 1) are recorded and the later steps still run.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
 OUT=$ROOT/gpurun_out
@@ -12,7 +12,7 @@ ok_or_stop() {  # $1 = exit code, $2 = step name
   echo "[$2] exit $rc" | tee -a "$OUT/steps.log"
   if [ "$rc" -ne 0 ] && [ "$rc" -ne 1 ]; then echo "stopping after abnormal exit of $2"; exit "$rc"; fi
 }
-STEPS=${STEPS:-pytest,smoke,bench,prof}
+STEPS=${STEPS:-pytest,smoke,traffic,bench,prof}
 if [[ $STEPS == *pytest* ]]; then
   timeout -k 10 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   ok_or_stop $? pytest
@@ -21,14 +21,18 @@ if [[ $STEPS == *smoke* ]]; then
   timeout -k 10 300 python -c "import __graft_entry__ as g; g.smoke()" > "$OUT/smoke.log" 2>&1
   ok_or_stop $? smoke
 fi
+if [[ $STEPS == *traffic* ]]; then
+  timeout -k 10 900 python tools/pmc_traffic.py "$OUT/hbm_traffic.json" ${BENCH_ARGS:-} > "$OUT/traffic.log" 2>&1
+  ok_or_stop $? traffic
+fi
 if [[ $STEPS == *bench* ]]; then
-  timeout -k 10 600 python bench.py ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
+  timeout -k 10 600 python bench.py --traffic-json "$OUT/hbm_traffic.json" ${BENCH_ARGS:-} > "$OUT/bench.log" 2>&1
   ok_or_stop $? bench
 fi
 if [[ $STEPS == *prof* ]]; then
   cd /tmp
   timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1
+    python3 "$ROOT/bench.py" --no-cpu-baseline --traffic-json "$OUT/hbm_traffic.json" ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1
   ok_or_stop $? prof
 fi
 exit 0
