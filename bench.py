@@ -172,11 +172,7 @@ def main():
 
 
 def kernel_name(variant, scene):
-    if variant == 1:
-        return "trace_grid_kernel"
-    if variant == 2 or (variant == 0 and not scene.info()["lds_locator_bytes"]):
-        return "trace_persistent_kernel"
-    return "trace_persistent_lds_kernel"
+    return {1: "trace_grid_kernel", 3: "trace_persistent_lds_kernel"}.get(variant, "trace_persistent_kernel")
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):

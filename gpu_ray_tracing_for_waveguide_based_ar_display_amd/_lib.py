@@ -16,7 +16,8 @@ LIB_PATH = os.path.join(PKG, "libwgrt.so")
 
 ABI_VERSION = 1
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
-            "wgrt_trace_fullcolor_ex", "wgrt_scene_classify", "wgrt_selftest_math", "wgrt_status_string",
+            "wgrt_trace_fullcolor_ex", "wgrt_scene_classify", "wgrt_locator_classify_host",
+            "wgrt_selftest_math", "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
 
@@ -95,6 +96,9 @@ def load(path: str = LIB_PATH):
                                           _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]
     L.wgrt_scene_classify.restype = st
     L.wgrt_scene_classify.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
+    L.wgrt_locator_classify_host.restype = st
+    L.wgrt_locator_classify_host.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_double, ctypes.c_int, _vp,
+                                             ctypes.c_int64, _vp]
     L.wgrt_selftest_math.restype = st
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_status_string.restype = ctypes.c_char_p
@@ -118,6 +122,57 @@ def _ptr(a: np.ndarray, t=_d):
     return a.ctypes.data_as(t)
 
 
+def make_desc(IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
+          lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2, lut_TIR, lut_gap):
+    """Validate the reference's scene arrays and pack them into a ``wgrt_scene_desc``.
+
+    Returns ``(desc, keepalive, (num_lmd, nx, ny, n_fc_slices, n_oc_slices))``; keep the
+    second item alive while the descriptor is in use.  Raises ValueError on any shape
+    mismatch (the reference would index out of bounds instead).
+    """
+    f64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.float64)
+    c128 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.complex128)
+    i64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.int64)
+    k = dict(IC=f64(IC), FC=f64(FC), FC_offset=i64(FC_offset), OC=f64(OC), OC_offset=i64(OC_offset),
+             eff1=f64(eff_reg1), eff2=f64(eff_reg2), fov=f64(eff_reg_FOV), fovr=f64(eff_reg_FOV_range),
+             ic1=c128(lut_ic1), ic2=c128(lut_ic2), ic3=c128(lut_ic3), fc1=c128(lut_fc1),
+             fc2=c128(lut_fc2), oc1=c128(lut_oc1), oc2=c128(lut_oc2), tir=f64(lut_TIR), gap=f64(lut_gap))
+    for name in ("IC", "FC", "OC", "eff1", "eff2"):
+        a = k[name]
+        if a.ndim != 2 or a.shape[1] != 2:
+            raise ValueError(f"{name} must have shape (V, 2), got {a.shape}")
+    if k["tir"].ndim != 4 or k["tir"].shape[-1] != 4:
+        raise ValueError(f"lut_TIR must have shape (L, NX, NY, 4), got {k['tir'].shape}")
+    nl, nx, ny = k["tir"].shape[:3]
+    nfc, noc = k["FC_offset"].shape[0] - 1, k["OC_offset"].shape[0] - 1
+    want = {"gap": (nl, nx, ny, 8), "fov": (nx, ny, 4, 2), "fovr": (nx, ny, 4)}
+    for name, shp in want.items():
+        if k[name].shape != shp:
+            raise ValueError(f"{name}: shape {k[name].shape} != {shp}")
+    for name in ("ic1", "ic2", "ic3"):
+        if k[name].shape[:3] != (nl, nx, ny):
+            raise ValueError(f"lut_{name}: shape {k[name].shape} does not match grid {(nl, nx, ny)}")
+    for name, ns in (("fc1", nfc), ("fc2", nfc), ("oc1", noc), ("oc2", noc)):
+        if k[name].shape[:4] != (ns, nl, nx, ny):
+            raise ValueError(f"lut_{name}: shape {k[name].shape} does not match {(ns, nl, nx, ny)}")
+    if k["FC_offset"][-1] > k["FC"].shape[0] or k["OC_offset"][-1] > k["OC"].shape[0]:
+        raise ValueError("FC_offset / OC_offset point past the vertex arrays")
+    ch5 = k["ic1"].shape[-1]
+    if not (k["ic2"].shape[-1] == k["ic3"].shape[-1] == k["oc1"].shape[-1] == k["oc2"].shape[-1] == ch5):
+        raise ValueError("ic*/oc* LUTs must share one channel count")
+    ch3 = k["fc1"].shape[-1]
+    if k["fc2"].shape[-1] != ch3:
+        raise ValueError("fc1/fc2 LUTs must share one channel count")
+    desc = SceneDesc(
+        _ptr(k["IC"]), k["IC"].shape[0], _ptr(k["FC"]), _ptr(k["FC_offset"], _i64), nfc,
+        _ptr(k["OC"]), _ptr(k["OC_offset"], _i64), noc, float(n_g),
+        _ptr(k["eff1"]), k["eff1"].shape[0], _ptr(k["eff2"]), k["eff2"].shape[0],
+        _ptr(k["fov"]), _ptr(k["fovr"]),
+        _ptr(k["ic1"]), _ptr(k["ic2"]), _ptr(k["ic3"]), _ptr(k["fc1"]), _ptr(k["fc2"]),
+        _ptr(k["oc1"]), _ptr(k["oc2"]), ch5, ch3, _ptr(k["tir"]), _ptr(k["gap"]), nl, nx, ny)
+    return desc, k, (nl, nx, ny, nfc, noc)
+
+
 class Scene:
     """Device-resident geometry + packed LUT tiles (``wgrt_scene_create``).
 
@@ -129,46 +184,9 @@ class Scene:
                  eff_reg_FOV_range, lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2,
                  lut_TIR, lut_gap, device: int = 0):
         L = load()
-        f64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.float64)
-        c128 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.complex128)
-        i64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.int64)
-        k = dict(IC=f64(IC), FC=f64(FC), FC_offset=i64(FC_offset), OC=f64(OC), OC_offset=i64(OC_offset),
-                 eff1=f64(eff_reg1), eff2=f64(eff_reg2), fov=f64(eff_reg_FOV), fovr=f64(eff_reg_FOV_range),
-                 ic1=c128(lut_ic1), ic2=c128(lut_ic2), ic3=c128(lut_ic3), fc1=c128(lut_fc1),
-                 fc2=c128(lut_fc2), oc1=c128(lut_oc1), oc2=c128(lut_oc2), tir=f64(lut_TIR), gap=f64(lut_gap))
-        for name in ("IC", "FC", "OC", "eff1", "eff2"):
-            a = k[name]
-            if a.ndim != 2 or a.shape[1] != 2:
-                raise ValueError(f"{name} must have shape (V, 2), got {a.shape}")
-        if k["tir"].ndim != 4 or k["tir"].shape[-1] != 4:
-            raise ValueError(f"lut_TIR must have shape (L, NX, NY, 4), got {k['tir'].shape}")
-        nl, nx, ny = k["tir"].shape[:3]
-        nfc, noc = k["FC_offset"].shape[0] - 1, k["OC_offset"].shape[0] - 1
-        want = {"gap": (nl, nx, ny, 8), "fov": (nx, ny, 4, 2), "fovr": (nx, ny, 4)}
-        for name, shp in want.items():
-            if k[name].shape != shp:
-                raise ValueError(f"{name}: shape {k[name].shape} != {shp}")
-        for name in ("ic1", "ic2", "ic3"):
-            if k[name].shape[:3] != (nl, nx, ny):
-                raise ValueError(f"lut_{name}: shape {k[name].shape} does not match grid {(nl, nx, ny)}")
-        for name, ns in (("fc1", nfc), ("fc2", nfc), ("oc1", noc), ("oc2", noc)):
-            if k[name].shape[:4] != (ns, nl, nx, ny):
-                raise ValueError(f"lut_{name}: shape {k[name].shape} does not match {(ns, nl, nx, ny)}")
-        if k["FC_offset"][-1] > k["FC"].shape[0] or k["OC_offset"][-1] > k["OC"].shape[0]:
-            raise ValueError("FC_offset / OC_offset point past the vertex arrays")
-        ch5 = k["ic1"].shape[-1]
-        if not (k["ic2"].shape[-1] == k["ic3"].shape[-1] == k["oc1"].shape[-1] == k["oc2"].shape[-1] == ch5):
-            raise ValueError("ic*/oc* LUTs must share one channel count")
-        ch3 = k["fc1"].shape[-1]
-        if k["fc2"].shape[-1] != ch3:
-            raise ValueError("fc1/fc2 LUTs must share one channel count")
-        desc = SceneDesc(
-            _ptr(k["IC"]), k["IC"].shape[0], _ptr(k["FC"]), _ptr(k["FC_offset"], _i64), nfc,
-            _ptr(k["OC"]), _ptr(k["OC_offset"], _i64), noc, float(n_g),
-            _ptr(k["eff1"]), k["eff1"].shape[0], _ptr(k["eff2"]), k["eff2"].shape[0],
-            _ptr(k["fov"]), _ptr(k["fovr"]),
-            _ptr(k["ic1"]), _ptr(k["ic2"]), _ptr(k["ic3"]), _ptr(k["fc1"]), _ptr(k["fc2"]),
-            _ptr(k["oc1"]), _ptr(k["oc2"]), ch5, ch3, _ptr(k["tir"]), _ptr(k["gap"]), nl, nx, ny)
+        desc, _keep, (nl, nx, ny, nfc, noc) = make_desc(
+            IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
+            lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2, lut_TIR, lut_gap)
         h = _vp()
         check(L.wgrt_scene_create(ctypes.byref(desc), int(device), ctypes.byref(h)), "wgrt_scene_create")
         self._h = h
@@ -208,3 +226,20 @@ class Scene:
             self.close()
         except Exception:
             pass
+
+
+def locator_classify_host(geom, luts, xy: np.ndarray, cell_mm: float = 0.125, which: int = 0) -> np.ndarray:
+    """Host replica of the kernels' polygon locator (``wgrt_locator_classify_host``): bit k of
+    the result is is_inside_or_on_edge(point, polygon k) (0 eff_reg1, 1 eff_reg2, 2 IC,
+    3.. FC slices, then OC slices).  Needs no GPU."""
+    L = load()
+    desc, keep, _ = make_desc(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g,
+                              geom.eff_reg1, geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range,
+                              luts["lut_ic1"], luts["lut_ic2"], luts["lut_ic3"], luts["lut_fc1"],
+                              luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"], geom.lut_TIR, geom.lut_gap)
+    pts = np.ascontiguousarray(xy, dtype=np.float64)
+    out = np.zeros(pts.shape[0], dtype=np.uint64)
+    check(L.wgrt_locator_classify_host(ctypes.byref(desc), float(cell_mm), int(which),
+                                       pts.ctypes.data_as(_vp), pts.shape[0], out.ctypes.data_as(_vp)),
+          "wgrt_locator_classify_host")
+    return out

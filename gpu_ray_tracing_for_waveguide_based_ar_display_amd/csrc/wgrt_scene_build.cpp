@@ -104,8 +104,8 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
         xmax = ymax = 1.0;
     }
     double h = cell_mm;
-    // keep the grid below ~4M cells whatever the coordinate range
-    while (((xmax - xmin) / h + 5) * ((ymax - ymin) / h + 5) > 4.0e6) h *= 2.0;
+    // keep the grid below ~16M cells (128 MB of 64-bit words) whatever the coordinate range
+    while (((xmax - xmin) / h + 5) * ((ymax - ymin) / h + 5) > 1.6e7) h *= 2.0;
     const double x0 = std::floor(xmin / h) * h - 2 * h;
     const double y0 = std::floor(ymin / h) * h - 2 * h;
     const int ncx = (int)std::ceil((xmax - x0) / h) + 3;
@@ -135,45 +135,69 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
             out.row_off[(size_t)k * ncy + cy + 1] = (int32_t)out.row_edges.size();
         }
     }
+    std::vector<double> xs;
     for (int k = 0; k < np; ++k) {
         std::fill(edge.begin(), edge.end(), 0);
         const double *xy = polys[k];
         const int64_t nv = nverts[k];
+        const double pad2 = 2 * kPad;
+        // (1) EDGE cells, row by row: the cells of row cy (expanded by pad2) that the edge's
+        //     part inside the row's y-range (expanded by pad2) can reach, widened by pad2.
         for (int64_t i = 0, j = nv - 1; i < nv; j = i++) {
             const double ax = xy[2 * j], ay = xy[2 * j + 1], bx = xy[2 * i], by = xy[2 * i + 1];
             const double len = std::hypot(bx - ax, by - ay);
-            const double pad2 = 2 * kPad;
-            const double ex0 = std::min(ax, bx) - pad2, ex1 = std::max(ax, bx) + pad2;
             const double ey0 = std::min(ay, by) - pad2, ey1 = std::max(ay, by) + pad2;
-            const int cx0 = std::max(0, (int)std::floor((ex0 - x0) / h) - 1);
-            const int cx1 = std::min(ncx - 1, (int)std::floor((ex1 - x0) / h) + 1);
             const int cy0 = std::max(0, (int)std::floor((ey0 - y0) / h) - 1);
             const int cy1 = std::min(ncy - 1, (int)std::floor((ey1 - y0) / h) + 1);
             for (int cy = cy0; cy <= cy1; ++cy) {
-                for (int cx = cx0; cx <= cx1; ++cx) {
-                    // cell expanded by kPad (covers index rounding), then by the margin kPad
-                    const double rx0 = x0 + cx * h - pad2, rx1 = x0 + (cx + 1) * h + pad2;
-                    const double ry0 = y0 + cy * h - pad2, ry1 = y0 + (cy + 1) * h + pad2;
-                    bool hit;
-                    if (len < kShortEdge) {
-                        hit = !(ex1 < rx0 || ex0 > rx1 || ey1 < ry0 || ey0 > ry1);
-                    } else {
-                        hit = segment_hits_rect(ax, ay, bx, by, rx0, rx1, ry0, ry1);
-                    }
-                    if (hit) edge[(size_t)cy * ncx + cx] = 1;
+                const double ry0 = y0 + cy * h - pad2, ry1 = y0 + (cy + 1) * h + pad2;
+                double lo, hi;
+                if (len < kShortEdge || std::fabs(by - ay) < 1e-300) {
+                    if (ey1 < ry0 || ey0 > ry1) continue;
+                    lo = std::min(ax, bx);
+                    hi = std::max(ax, bx);
+                } else {
+                    // parameter range of the segment inside [ry0, ry1]
+                    double t0 = (ry0 - ay) / (by - ay), t1 = (ry1 - ay) / (by - ay);
+                    if (t0 > t1) std::swap(t0, t1);
+                    t0 = std::max(t0, 0.0);
+                    t1 = std::min(t1, 1.0);
+                    if (t0 > t1 + 1e-12) continue;
+                    const double xa = ax + t0 * (bx - ax), xb = ax + t1 * (bx - ax);
+                    lo = std::min(xa, xb);
+                    hi = std::max(xa, xb);
                 }
+                lo -= pad2 + 1e-9;
+                hi += pad2 + 1e-9;
+                const int cx0 = std::max(0, (int)std::floor((lo - x0) / h));
+                const int cx1 = std::min(ncx - 1, (int)std::floor((hi - x0) / h));
+                for (int cx = cx0; cx <= cx1; ++cx) edge[(size_t)cy * ncx + cx] = 1;
             }
         }
+        // (2) IN / OUT of the other cells: the reference predicate at the cell centre,
+        //     evaluated for a whole row at once.  At a non-EDGE centre no edge is on-edge
+        //     (bounding box), so the predicate is the crossing parity; the crossings of the
+        //     row-centre line are computed with the reference's own expression (GRTF:47) and
+        //     counted against the centres in one sweep.
         for (int cy = 0; cy < ncy; ++cy) {
+            const double py = y0 + (cy + 0.5) * h;
+            xs.clear();
+            for (int64_t i = 0, j = nv - 1; i < nv; j = i++) {
+                const double xi = xy[2 * i], yi = xy[2 * i + 1], xj = xy[2 * j], yj = xy[2 * j + 1];
+                if ((yi > py) != (yj > py)) xs.push_back((xj - xi) * (py - yi) / (yj - yi + 1e-20) + xi);
+            }
+            std::sort(xs.begin(), xs.end());
+            size_t le = 0;   // crossings with xint <= px
             for (int cx = 0; cx < ncx; ++cx) {
                 const size_t c = (size_t)cy * ncx + cx;
+                const double px = x0 + (cx + 0.5) * h;
+                while (le < xs.size() && !(px < xs[le])) ++le;
                 uint64_t cls;
                 if (edge[c]) {
                     cls = 2;
                     ++out.edge_cells;
                 } else {
-                    const double px = x0 + (cx + 0.5) * h, py = y0 + (cy + 0.5) * h;
-                    cls = inside_or_on_edge(px, py, xy, (int)nv) ? 1 : 0;
+                    cls = ((xs.size() - le) & 1u) ? 1 : 0;   // parity of crossings with px < xint
                 }
                 out.cells[c] |= cls << (2 * k);
             }

@@ -27,7 +27,9 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <algorithm>
 #include <atomic>
+#include <cmath>
 #include <mutex>
 #include <string>
 #include <vector>
@@ -45,6 +47,12 @@ thread_local std::string g_last_error;
 // step (env WGRT_MAX_HOPS, 0 = unbounded).  Bounding it keeps lanes whose ray is crossing a
 // coupler-free stretch from stalling the whole wave; 2 measured best on the C3 workload
 // (0.92 ms vs 1.05 ms unbounded, tools/ab.py).  Scheduling only: results are identical.
+// Cell size (mm) of the global-memory locator grid (env WGRT_CELL_MM); the LDS copy uses
+// the smallest power-of-two multiple of twice this size that fits the LDS budget.
+double g_cell_mm = [] {
+    const char *v = getenv("WGRT_CELL_MM");
+    return v ? atof(v) : 0.015625;   // 1/64 mm: 37 MB grid at the reference design; fastest on C3
+}();
 int g_max_hops = [] {
     const char *v = getenv("WGRT_MAX_HOPS");
     return v ? atoi(v) : 2;
@@ -109,6 +117,24 @@ constexpr int kPolyEff2 = 1;
 constexpr int kPolyIC = 2;
 constexpr int kPolyFC0 = 3;
 
+#ifdef WGRT_DIAG
+// Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
+__device__ unsigned long long g_diag[16];
+__device__ unsigned long long g_diag_fallback;
+// region r: g_diag[6 + r] += number of wave executions, g_diag_act[r] += active lanes
+__device__ unsigned long long g_diag_act[16];
+__device__ __forceinline__ void diag_region(int r) {
+    const uint64_t m = __ballot(1);
+    if ((threadIdx.x & 63) == __builtin_ctzll(m)) {
+        atomicAdd(&g_diag[6 + r], 1ull);
+        atomicAdd(&g_diag_act[r], (unsigned long long)__popcll(m));
+    }
+}
+#define DIAG_REGION(r) diag_region(r)
+#else
+#define DIAG_REGION(r) ((void)0)
+#endif
+
 // A point's cell of the locator grid: the per-polygon class word and the cell row.
 struct Cell {
     uint64_t w;
@@ -131,6 +157,7 @@ template <class Loc>
 __device__ __forceinline__ bool in_poly(const Loc &L, const Cell &c, int k, double x, double y) {
     const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
+    DIAG_REGION(4);   // exact EDGE-cell test
     const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
     const int r = k * L.ncy + c.cy;
     const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
@@ -178,10 +205,24 @@ __device__ __forceinline__ Field efield(double Ete, double Etm, double cd, doubl
 
 // Output phase difference of E_field_cal: wrap(atan2(Etm') - atan2(Ete')), 0 phase for a
 // component with |.| < 1e-20 (GRTF:147-150).
+// The two atan2 run as two trips of one non-unrolled loop: one copy of the (register-hungry)
+// f64 atan2 body instead of two interleaved ones keeps the kernel's VGPR peak down.
 __device__ __forceinline__ double efield_phase(const Field &f, double te, double tm) {
-    const double pte = (te >= 1e-20) ? atan2(f.te_im, f.te_re) : 0.0;
-    const double ptm = (tm >= 1e-20) ? atan2(f.tm_im, f.tm_re) : 0.0;
-    return wrap_pi(ptm - pte);
+    double ph[2] = {0.0, 0.0};
+#pragma unroll 1
+    for (int k = 0; k < 2; ++k) {
+        const double y = k == 0 ? f.te_im : f.tm_im;
+        const double x = k == 0 ? f.te_re : f.tm_re;
+        const double mag = k == 0 ? te : tm;
+#ifdef WGRT_ABL_ATAN2
+        const double a = (mag >= 1e-20) ? y * x : 0.0;   // ablation build only
+#else
+        const double a = (mag >= 1e-20) ? atan2(y, x) : 0.0;
+#endif
+        if (k == 0) ph[0] = a;
+        else ph[1] = a;
+    }
+    return wrap_pi(ph[1] - ph[0]);
 }
 
 struct Ray {
@@ -203,21 +244,30 @@ struct Lane {
 // Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
 // FoV / wavelength indices fall outside the scene.
 __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L) {
-    const int m = (int)A.m[i], n = (int)A.n[i], l = (int)A.l[i];
+#ifdef WGRT_ABL_RAYLOAD
+    const int64_t ld = i & 1023;   // ablation build only: ray inputs from a cache-hot window
+#else
+    const int64_t ld = i;
+#endif
+    const int m = (int)A.m[ld], n = (int)A.n[ld], l = (int)A.l[ld];
     if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
     L.i = i;
     L.l = l;
     L.m = m;
     L.n = n;
+#ifdef WGRT_ABL_TILE
+    L.T = A.tiles;   // ablation build only: every ray reads tile 0 (L1-resident)
+#else
     L.T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
-    L.r.x = (double)A.x[i];
-    L.r.y = (double)A.y[i];
-    L.r.te = (double)A.te[i];
-    L.r.tm = (double)A.tm[i];
-    L.r.dph = (double)A.dph[i];
+#endif
+    L.r.x = (double)A.x[ld];
+    L.r.y = (double)A.y[ld];
+    L.r.te = (double)A.te[ld];
+    L.r.tm = (double)A.tm[ld];
+    L.r.dph = (double)A.dph[ld];
     L.r.cos_t = 1.0;
     L.r.ener = 1.0;
-    L.r.s = A.rng[i];
+    L.r.s = A.rng[ld];
     L.r.region = 0;
     L.bounces = 1;
     L.hit = false;
@@ -226,11 +276,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
 
 enum : int { kDie = -1, kTransit = -2 };
 
-#ifdef WGRT_DIAG
-// Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
-__device__ unsigned long long g_diag[16];
-__device__ unsigned long long g_diag_fallback;
-#endif
+
 
 // A coupler interaction: `blk` of the lane's tile, `kind` 0 in-coupler states (entry event,
 // R0, R1), 1 R2, 2 R3, 3 R4, 4 R5.  Evaluates every branch's efficiency (GRTF:860-869,
@@ -243,8 +289,14 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     Ray &r = L.r;
     const double *T = L.T;
     const double *B = T + kTileHeader + kBlock * blk;
+    DIAG_REGION(0);   // interaction
     double sd, cd;
+#ifdef WGRT_ABL_SINCOS
+    sd = r.dph * 0.5;   // ablation build only
+    cd = 1.0 - r.dph * 0.25;
+#else
     sincos(r.dph, &sd, &cd);
+#endif
     const bool three = kind >= 3;
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
     const double denom = entry ? T[kTileCosIc1] : r.cos_t;
@@ -317,6 +369,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     }
 
     if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
+        DIAG_REGION(2);
         if (inside_or_on_edge(r.x, r.y, T + kTileEbRect, 4)) {
             const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
             const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
@@ -336,6 +389,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         }
         return kDie;
     }
+    DIAG_REGION(1);   // take a branch
     const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * b);
     const double cte = hypot_cr(f.te_re, f.te_im);
     const double ctm = hypot_cr(f.tm_re, f.tm_im);
@@ -356,6 +410,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
     if (kind == 0) {
+        DIAG_REGION(5);
         const bool in_ic = in_poly(loc, locate(loc, r.x, r.y), kPolyIC, r.x, r.y);
         if (b == 0) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
@@ -380,6 +435,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     const double dtir = 2 * T[kTileTir + (g >> 1)];
     for (int hops = 0;; ++hops) {
         if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
+        DIAG_REGION(3);   // loop iteration in advance
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
         const Cell c = locate(loc, r.x, r.y);
@@ -529,6 +585,7 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
             if (!active) {
                 const int rank = __popcll(need & lt_mask);
                 if (rank < take) {
+                    DIAG_REGION(6);
                     if (lane_load(A, cur + rank, L)) {
                         active = true;
                         blk = 0;
@@ -704,7 +761,7 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     *out = nullptr;
     SceneHost host;
     try {
-        build_scene_host(*desc, 0.125, host);
+        build_scene_host(*desc, g_cell_mm, host);
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
@@ -848,7 +905,7 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
         if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
         hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
     } else {
-        const bool use_lds = variant == 3 || (variant == 0 && s->lds_grid > 0);
+        const bool use_lds = variant == 3;
         if (use_lds && s->lds_grid == 0)
             return fail(WGRT_ERR_UNSUPPORTED, "variant 3 needs the locator to fit in LDS (<= 16 polygons)");
         wgrt_scene *ms = const_cast<wgrt_scene *>(s);
@@ -909,6 +966,67 @@ wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, doub
     return WGRT_OK;
 }
 
+wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, int which, const double *xy,
+                                       int64_t n, uint64_t *out_mask) {
+    if (!desc || (n > 0 && (!xy || !out_mask))) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (!(cell_mm > 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be > 0");
+    SceneHost host;
+    try {
+        build_scene_host(*desc, cell_mm, host);
+    } catch (const std::exception &e) {
+        return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
+    }
+    const int npoly = (int)host.loc.poly_off.size() - 1;
+    if (which == 1 && !host.lds.ok) return fail(WGRT_ERR_UNSUPPORTED, "no LDS locator image for this scene");
+    // host replica of the device locator (same arithmetic as locate / in_poly)
+    LocatorT<uint64_t> g{};
+    std::vector<uint64_t> cells64;
+    if (which == 0) {
+        g.cells = host.loc.cells.data();
+        g.verts = host.loc.verts.data();
+        g.poly_off = host.loc.poly_off.data();
+        g.row_off = host.loc.row_off.data();
+        g.row_edges = host.loc.row_edges.data();
+        g.x0 = host.loc.x0, g.y0 = host.loc.y0, g.inv_h = host.loc.inv_h, g.ncx = host.loc.ncx, g.ncy = host.loc.ncy;
+    } else {
+        const LdsImage &I = host.lds;
+        const char *b = I.bytes.data();
+        const size_t ncell = (size_t)I.ncx * I.ncy;
+        cells64.resize(ncell);
+        for (size_t k = 0; k < ncell; ++k) cells64[k] = ((const uint32_t *)(b + I.off_cells))[k];
+        g.cells = cells64.data();
+        g.verts = (const double *)(b + I.off_verts);
+        g.poly_off = (const int32_t *)(b + I.off_poly);
+        g.row_off = (const int32_t *)(b + I.off_row_off);
+        g.row_edges = (const int32_t *)(b + I.off_row_edges);
+        g.x0 = I.x0, g.y0 = I.y0, g.inv_h = I.inv_h, g.ncx = I.ncx, g.ncy = I.ncy;
+    }
+    for (int64_t i = 0; i < n; ++i) {
+        const double x = xy[2 * i], y = xy[2 * i + 1];
+        const double fx = std::floor((x - g.x0) * g.inv_h), fy = std::floor((y - g.y0) * g.inv_h);
+        uint64_t w = 0;
+        int cy = 0;
+        if (fx >= 0.0 && fy >= 0.0 && fx < (double)g.ncx && fy < (double)g.ncy) {
+            cy = (int)fy;
+            w = g.cells[(size_t)cy * g.ncx + (int)fx];
+        }
+        uint64_t mask = 0;
+        for (int k = 0; k < npoly; ++k) {
+            const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
+            bool in = cls == 1u;
+            if (cls == 2u) {
+                const int a = g.poly_off[k], nv = g.poly_off[k + 1] - a;
+                const int r = k * g.ncy + cy;
+                in = inside_or_on_edge_subset(x, y, g.verts + 2 * a, nv, g.row_edges + g.row_off[r],
+                                              g.row_off[r + 1] - g.row_off[r]);
+            }
+            if (in) mask |= 1ull << k;
+        }
+        out_mask[i] = mask;
+    }
+    return WGRT_OK;
+}
+
 const char *wgrt_status_string(wgrt_status s) {
     switch (s) {
         case WGRT_OK: return "ok";
@@ -926,6 +1044,13 @@ int wgrt_abi_version(void) { return WGRT_ABI_VERSION; }
 
 #ifdef WGRT_DIAG
 // Diagnostic build only: read-and-reset the wave-loop counters (synchronous).
+int wgrt_diag_read_regions(unsigned long long *out16) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_diag_act), 16 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_act), z, sizeof(z));
+    return 0;
+}
+
 int wgrt_diag_read(unsigned long long *out17) {
     unsigned long long h[16], fb = 0;
     if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) != hipSuccess) return 2;

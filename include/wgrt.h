@@ -125,8 +125,8 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
 /* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
  * count for the persistent variant (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
  * grid, 2 persistent wave-refill (locator in global memory), 3 persistent wave-refill with
- * the locator staged in LDS (needs <= 16 polygons; WGRT_ERR_UNSUPPORTED otherwise).  Auto
- * picks 3 when available, else 2.  All variants produce identical results. */
+ * a coarser copy of the locator staged in LDS (needs <= 16 polygons; WGRT_ERR_UNSUPPORTED
+ * otherwise).  Auto picks 2.  All variants produce identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
@@ -137,6 +137,12 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *ra
  * 0 eff_reg1, 1 eff_reg2, 2 IC, 3.. FC slices, then OC slices (GRTF:63-71).  Test hook. */
 wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64_t n,
                                 uint64_t *out_mask, void *stream);
+
+/* Host-only replica of the locator (no GPU needed; test hook): builds the scene's
+ * locator with cell size cell_mm (which = 0: the global-memory grid; 1: the LDS image)
+ * and classifies n HOST points exactly as the kernels do. */
+wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, int which, const double *xy,
+                                       int64_t n, uint64_t *out_mask);
 
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */

@@ -1,0 +1,50 @@
+"""The exact polygon locator (grid classes + row-band edge lists), through its host replica
+(wgrt_locator_classify_host -- the kernels' arithmetic, no GPU), must equal the reference
+predicate is_inside_or_on_edge (GRTF:63-71, via the oracle) on random and adversarial
+points, for the global grid at several cell sizes and for the LDS image."""
+import numpy as np
+import pytest
+
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd._lib import locator_classify_host
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+from oracle import inside_many
+
+
+@pytest.fixture(scope="module")
+def scene():
+    g = design_geometry(5, 4)
+    luts = synthetic_luts(g, seed=1)
+    polys = [g.eff_reg1, g.eff_reg2, g.IC] + \
+        [g.FC[g.FC_offset[k]:g.FC_offset[k + 1]] for k in range(len(g.FC_offset) - 1)] + \
+        [g.OC[g.OC_offset[k]:g.OC_offset[k + 1]] for k in range(len(g.OC_offset) - 1)]
+    rng = np.random.default_rng(0)
+    allv = np.concatenate(polys)
+    lo, hi = allv.min(0) - 1, allv.max(0) + 1
+    pts = [rng.uniform(lo, hi, size=(60000, 2))]
+    for P in polys:  # vertices, points on edges, and points 1e-13 .. 1e-5 off them
+        a, b = P, np.roll(P, -1, axis=0)
+        t = rng.uniform(0, 1, size=(len(P), 1))
+        on = a + t * (b - a)
+        pts += [a, on]
+        for d in (1e-13, 1e-12, 2e-12, 1e-9, 1e-7, 1e-6, 3e-6, 1e-5):
+            pts += [on + d * rng.standard_normal(on.shape), a + d * rng.standard_normal(a.shape)]
+    # points on the grid's own cell boundaries (multiples of the cell size)
+    for h in (0.25, 0.125, 0.03125):
+        gx = np.arange(np.floor(lo[0] / h), np.ceil(hi[0] / h)) * h
+        gy = rng.uniform(lo[1], hi[1], size=gx.shape)
+        pts += [np.stack([gx, gy], 1), np.stack([gy * 0 + gx[len(gx) // 2], gx * 0 + gy], 1)]
+    xy = np.ascontiguousarray(np.concatenate(pts))
+    want = np.zeros(len(xy), dtype=np.uint64)
+    for k, P in enumerate(polys):
+        want |= inside_many(xy, P).astype(np.uint64) << np.uint64(k)
+    return g, luts, xy, want
+
+
+@pytest.mark.parametrize("cell_mm,which", [(0.25, 0), (0.125, 0), (0.03125, 0), (0.125, 1)])
+def test_locator_equals_reference_predicate(scene, cell_mm, which):
+    g, luts, xy, want = scene
+    got = locator_classify_host(g, luts, xy, cell_mm=cell_mm, which=which)
+    bad = np.flatnonzero(got != want)
+    assert bad.size == 0, f"{bad.size} mismatches, e.g. {xy[bad[:3]]} got {got[bad[:3]]} want {want[bad[:3]]}"
+    assert want.any()

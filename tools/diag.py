@@ -43,6 +43,9 @@ L.wgrt_diag_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 buf = (ctypes.c_ulonglong * 17)()
 trace_fullcolor(scene, rays, rng, eb, stats=st, variant=variant)
 torch.cuda.synchronize()
+acts = (ctypes.c_ulonglong * 16)()
+L.wgrt_diag_read_regions.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+L.wgrt_diag_read_regions(acts)
 L.wgrt_diag_read(buf)
 d = list(buf)
 b = int(st[0])
@@ -51,3 +54,6 @@ print(f"passes={d[0]} mean_active_at_interact={d[1] / max(d[0], 1):.1f}/64 "
       f"passes_after_exhaust={d[2]} ({d[2] / max(d[0], 1):.1%}) mean_active_after={d[3] / max(d[2], 1):.1f}")
 print(f"lane_hops={d[4]} hops/pass(lane-mean)={d[4] / max(d[1], 1):.2f} simt_hop_cost/pass={d[5] / max(d[0], 1):.2f} "
       f"exact_fallbacks={d[16]} interactions~={d[1]}")
+for r, name in enumerate(["interact", "take", "eyebox", "advance-iter", "edge-test", "ic-check", "refill-load"]):
+    n, act = d[6 + r], acts[r]
+    print(f"  region {name:13s} wave-execs={n:9d} mean_active={act / max(n, 1):5.1f}/64")
