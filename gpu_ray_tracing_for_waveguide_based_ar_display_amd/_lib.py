@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG, "libwgrt.so")
 
 ABI_VERSION = 1
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
-            "wgrt_trace_fullcolor_ex", "wgrt_scene_classify", "wgrt_locator_classify_host",
+            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -94,6 +94,13 @@ def load(path: str = LIB_PATH):
     L.wgrt_trace_fullcolor_ex.restype = st
     L.wgrt_trace_fullcolor_ex.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, _vp,
                                           _vp, _vp, _vp, _vp, ctypes.c_int, ctypes.c_int]
+    L.wgrt_trace_single.restype = st
+    L.wgrt_trace_single.argtypes = L.wgrt_trace_fullcolor.argtypes
+    L.wgrt_trace_single_ex.restype = st
+    L.wgrt_trace_single_ex.argtypes = L.wgrt_trace_fullcolor_ex.argtypes
+    L.wgrt_rays_init.restype = st
+    L.wgrt_rays_init.argtypes = [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32,
+                                 ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(Rays), _vp, _vp]
     L.wgrt_scene_classify.restype = st
     L.wgrt_scene_classify.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_locator_classify_host.restype = st
@@ -127,9 +134,15 @@ def make_desc(IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg
     """Validate the reference's scene arrays and pack them into a ``wgrt_scene_desc``.
 
     Returns ``(desc, keepalive, (num_lmd, nx, ny, n_fc_slices, n_oc_slices))``; keep the
-    second item alive while the descriptor is in use.  Raises ValueError on any shape
+    second item alive while the descriptor is in use.  Single-wavelength LUTs (the
+    ``process_rays_kernel_pro`` shapes: lut_TIR [NX, NY, 4], lut_fc1 [nFC, NX, NY, C], ...)
+    are accepted and described as num_lmd = 1 (the same memory layout).  Raises ValueError on any shape
     mismatch (the reference would index out of bounds instead).
     """
+    if np.ndim(lut_TIR) == 3:   # single-wavelength LUTs (GRTF:419-427): add a lambda axis of 1
+        lut_ic1, lut_ic2, lut_ic3, lut_TIR, lut_gap = (np.asarray(a)[None] for a in
+                                                       (lut_ic1, lut_ic2, lut_ic3, lut_TIR, lut_gap))
+        lut_fc1, lut_fc2, lut_oc1, lut_oc2 = (np.asarray(a)[:, None] for a in (lut_fc1, lut_fc2, lut_oc1, lut_oc2))
     f64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.float64)
     c128 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.complex128)
     i64 = lambda a: np.ascontiguousarray(np.asarray(a), dtype=np.int64)
@@ -190,17 +203,24 @@ class Scene:
         h = _vp()
         check(L.wgrt_scene_create(ctypes.byref(desc), int(device), ctypes.byref(h)), "wgrt_scene_create")
         self._h = h
+        self.single_lambda = np.ndim(lut_TIR) == 3
         self.device = int(device)
         self.num_lmd, self.nx, self.ny = nl, nx, ny
         self.n_fc_slices, self.n_oc_slices = nfc, noc
         self.n_g = float(n_g)
 
     @classmethod
-    def from_geometry(cls, geom, luts: dict, device: int = 0):
+    def from_geometry(cls, geom, luts: dict, device: int = 0, wavelength: int | None = None):
+        """Scene of a geometry + LUT set.  ``wavelength=l`` builds the single-wavelength scene
+        of wavelength l (the arrays process_rays_kernel_pro takes, luts.single_wavelength)."""
+        tir, gap = geom.lut_TIR, geom.lut_gap
+        if wavelength is not None:
+            from .luts import single_wavelength
+            luts, tir, gap = single_wavelength(luts, tir, gap, wavelength)
         return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
                    geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts["lut_ic1"], luts["lut_ic2"],
                    luts["lut_ic3"], luts["lut_fc1"], luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"],
-                   geom.lut_TIR, geom.lut_gap, device=device)
+                   tir, gap, device=device)
 
     @property
     def handle(self):
@@ -214,6 +234,8 @@ class Scene:
         return {f: getattr(inf, f) for f, _ in SceneInfo._fields_}
 
     def eb_shape(self):
+        if self.single_lambda:   # process_rays_kernel_pro's matrix_EB [NY, NX, 80, 120]
+            return (self.ny, self.nx, 80, 120)
         return (self.num_lmd, self.ny, self.nx, 80, 120)
 
     def close(self):

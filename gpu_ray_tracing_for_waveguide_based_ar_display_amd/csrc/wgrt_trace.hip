@@ -109,6 +109,7 @@ struct TraceArgs {
     LdsLocatorDesc lds;
     int tile_d, nfc, noc, nx, ny, nl;
     double n_g, inv_n_g;
+    double threshold;   // ener * efficiency > threshold guard of R2..R5: 0 full colour, 1e-15 single lambda
     int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
 };
 
@@ -249,7 +250,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
 #else
     const int64_t ld = i;
 #endif
-    const int m = (int)A.m[ld], n = (int)A.n[ld], l = (int)A.l[ld];
+    const int m = (int)A.m[ld], n = (int)A.n[ld], l = A.l ? (int)A.l[ld] : 0;
     if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
     L.i = i;
     L.l = l;
@@ -332,13 +333,24 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     const double tol = 1e-12 * scale;
     const bool tiny = thr && !(r.ener > 1e-200 && (a0 == 0.0 || a0 > 1e-100) && (a1 == 0.0 || a1 > 1e-100) &&
                                (!three || a2 == 0.0 || a2 > 1e-100));
-    const bool sure = scale > 1e-290 && !tiny && fabs(u - c0) > tol && fabs(u - c1) > tol &&
+    // ener * e_k > threshold (GRTF:606 single-lambda: 1e-15; GRTF:1020 full colour: 0).  With
+    // threshold 0 and no underflow it is e_k > 0, i.e. a_k > 0; otherwise the estimate
+    // ener * a_k must clear the threshold by a relative margin far above its error.
+    const double t = A.threshold;
+    const double p0 = r.ener * a0, p1 = r.ener * a1, p2 = r.ener * a2;
+    const double tmar = 1e-12 * t;
+    const bool tsure = !thr || t == 0.0 ||
+                       (fabs(p0 - t) > tmar && fabs(p1 - t) > tmar && (!three || fabs(p2 - t) > tmar));
+    const bool pass0 = !thr || (t == 0.0 ? a0 > 0.0 : p0 > t);
+    const bool pass1 = !thr || (t == 0.0 ? a1 > 0.0 : p1 > t);
+    const bool pass2 = t == 0.0 ? a2 > 0.0 : p2 > t;
+    const bool sure = scale > 1e-290 && !tiny && tsure && fabs(u - c0) > tol && fabs(u - c1) > tol &&
                       (!three || fabs(u - c2) > tol);
     int b;
     if (sure) {
-        if (u <= c0 && (!thr || a0 > 0.0)) b = 0;
-        else if (u <= c1 && (!thr || a1 > 0.0)) b = 1;
-        else if (three && u <= c2 && a2 > 0.0) b = 2;
+        if (u <= c0 && pass0) b = 0;
+        else if (u <= c1 && pass1) b = 1;
+        else if (three && u <= c2 && pass2) b = 2;
         else return kDie;
     } else {
 #ifdef WGRT_DIAG
@@ -362,9 +374,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         }
         double e2 = 0.0;
         if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
-        if (u <= e0 && (!thr || r.ener * e0 > 0.0)) b = 0;
-        else if (u <= e0 + e1 && (!thr || r.ener * e1 > 0.0)) b = 1;
-        else if (three && u <= e0 + e1 + e2 && r.ener * e2 > 0.0) b = 2;
+        if (u <= e0 && (!thr || r.ener * e0 > t)) b = 0;
+        else if (u <= e0 + e1 && (!thr || r.ener * e1 > t)) b = 1;
+        else if (three && u <= e0 + e1 + e2 && r.ener * e2 > t) b = 2;
         else return kDie;
     }
 
@@ -643,6 +655,15 @@ __global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, u
     persistent_body(A, A.loc, counter, chunk);
 }
 
+// Variants 4-6: variant 2 at W waves per SIMD (W = 2: register budget 256, no VGPR spills)
+// and/or with 32-bit cell words in global memory (scenes of <= 16 polygons: half the
+// grid's cache footprint).
+template <class CellT, int W>
+__global__ __launch_bounds__(256, W) void trace_persistent_g_kernel(TraceArgs A, LocatorT<CellT> loc,
+                                                                    unsigned long long *counter, int chunk) {
+    persistent_body(A, loc, counter, chunk);
+}
+
 // Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
 // row-band edge lists) staged once into LDS by every workgroup, so the per-hop membership
 // tests cost LDS reads instead of dependent L2 round trips.  One 768-thread workgroup
@@ -683,6 +704,46 @@ __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, con
     out[i] = mask;
 }
 
+// Ray setup of FoV x wavelength blocks [blk_lo, blk_lo + n / R) (reference MAIN:65-115, 158):
+// ray i of block b = (ii * ny + jj) * nl + k takes origin point r = i % R (TE half) or
+// r - R/2 (TM half); m = ii, n = jj, lmd_num = lambdas[k]; gap / angles / phase 0.  With an
+// odd R the reference leaves the last ray of every block all-zero (its two halves cover
+// 2 * floor(R / 2) rays), and so does this.
+struct RayInitArgs {
+    const double *points;   // [R / 2, 2]
+    float *col[12];         // wgrt_ray_columns order, NULL = not written
+    uint32_t *rng;
+    int64_t n, R, blk_lo, gid_offset;
+    int ny, nl;
+    float lambdas[8];
+};
+
+__global__ __launch_bounds__(256) void rays_init_kernel(RayInitArgs A) {
+    const int64_t half = A.R / 2;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n;
+         i += (int64_t)gridDim.x * blockDim.x) {
+        const int64_t blk = A.blk_lo + i / A.R, r = i % A.R;
+        const int k = (int)(blk % A.nl);
+        const int64_t fov = blk / A.nl;
+        const int jj = (int)(fov % A.ny), ii = (int)(fov / A.ny);
+        float v[12] = {0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f, 0.f};
+        if (r < 2 * half) {
+            const int64_t p = r < half ? r : r - half;
+            v[0] = (float)A.points[2 * p];       // x    (float64 -> float32, round to nearest)
+            v[1] = (float)A.points[2 * p + 1];   // y
+            v[6] = (float)ii;                    // m
+            v[7] = (float)jj;                    // n
+            v[8] = A.lambdas[k];                 // lmd_num
+            v[9] = r < half ? 1.f : 0.f;         // te
+            v[10] = r < half ? 0.f : 1.f;        // tm
+        }
+#pragma unroll
+        for (int c = 0; c < 12; ++c)
+            if (A.col[c]) A.col[c][i] = v[c];
+        if (A.rng) A.rng[i] = 0x9E3779B9u * (uint32_t)(A.gid_offset + i + 1);   // MAIN:158, mod 2^32
+    }
+}
+
 __global__ __launch_bounds__(256) void selftest_math_kernel(const double *a, const double *b, int64_t n,
                                                             double *out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -707,6 +768,7 @@ struct wgrt_scene {
     double n_g = 0;
     double *d_tiles = nullptr;
     uint64_t *d_cells = nullptr;
+    uint32_t *d_cells32 = nullptr;   // 32-bit copy of the cell words (npoly <= 16), else NULL
     double *d_verts = nullptr;
     int32_t *d_poly_off = nullptr;
     int32_t *d_row_off = nullptr;
@@ -719,6 +781,7 @@ struct wgrt_scene {
     unsigned long long *d_counters = nullptr;
     std::atomic<unsigned> next_counter{0};
     int persistent_grid = 0;   // resident 256-thread workgroups of variant 2
+    int persistent_w2_grid = 0;   // ... of variant 4
     int lds_grid = 0;          // resident 768-thread workgroups of variant 3 (0: unavailable)
     char *d_lds_image = nullptr;
     size_t lds_bytes = 0;
@@ -786,6 +849,13 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         wgrt_scene_destroy(s);
         return st;
     }
+    if (s->npoly <= 16) {
+        std::vector<uint32_t> c32(host.loc.cells.begin(), host.loc.cells.end());
+        if ((st = upload(c32, &s->d_cells32)) != WGRT_OK) {
+            wgrt_scene_destroy(s);
+            return st;
+        }
+    }
     {
         hipError_t e = hipMalloc((void **)&s->d_counters, sizeof(unsigned long long) * wgrt_scene::kCounterSlots);
         if (e != hipSuccess) {
@@ -796,6 +866,8 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_kernel, 256, 0));
         s->persistent_grid = std::max(1, cus * std::max(1, per_cu));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_g_kernel<uint64_t, 2>, 256, 0));
+        s->persistent_w2_grid = std::max(1, cus * std::max(1, per_cu));
         if (host.lds.ok) {
             const int bytes = (int)host.lds.bytes.size();
             int lds_max = 0;
@@ -836,6 +908,7 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipSetDevice(s->device);
     (void)hipFree(s->d_tiles);
     (void)hipFree(s->d_cells);
+    (void)hipFree(s->d_cells32);
     (void)hipFree(s->d_verts);
     (void)hipFree(s->d_poly_off);
     (void)hipFree(s->d_counters);
@@ -861,23 +934,31 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     return WGRT_OK;
 }
 
-wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays,
-                                    int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
-                                    wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
-                                    int variant, int workgroups) {
+// One launch of the bounce kernel.  single: the single-wavelength kernel
+// process_rays_kernel_pro (GRTF:419-831) -- no lmd_num column, wavelength 0 of a
+// one-wavelength scene, threshold 1e-15; otherwise process_rays_kernel_pro_fullColor
+// (GRTF:833-1246), threshold 0.  The two kernels differ in nothing else.
+static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                                uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                                uint32_t *per_ray_bounces, void *stream, int variant, int workgroups, bool single) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
+    if (single && s->nl != 1)
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "single-wavelength trace needs a scene built with num_lmd == 1");
     if (n_rays == 0) return WGRT_OK;
-    if (!rays->x || !rays->y || !rays->m || !rays->n || !rays->lmd_num || !rays->te || !rays->tm ||
+    if (!rays->x || !rays->y || !rays->m || !rays->n || (!single && !rays->lmd_num) || !rays->te || !rays->tm ||
         !rays->delta_phase || !rng_states || !matrix_EB)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL ray column / rng_states / matrix_EB");
-    if (variant < 0 || variant > 3) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+    if (variant < 0 || variant > 6) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+    if ((variant == 5 || variant == 6) && !s->d_cells32)
+        return fail(WGRT_ERR_UNSUPPORTED, "variants 5 / 6 need <= 16 polygons");
     TraceArgs A;
     A.x = rays->x;
     A.y = rays->y;
     A.m = rays->m;
     A.n = rays->n;
-    A.l = rays->lmd_num;
+    A.l = single ? nullptr : rays->lmd_num;
+    A.threshold = single ? 1e-15 : 0.0;
     A.te = rays->te;
     A.tm = rays->tm;
     A.dph = rays->delta_phase;
@@ -912,7 +993,10 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
         unsigned long long *ctr = ms->d_counters + (ms->next_counter++ % wgrt_scene::kCounterSlots);
         HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st));
         const int tpb = use_lds ? 768 : 256;
-        int64_t grid = workgroups > 0 ? workgroups : (use_lds ? s->lds_grid : s->persistent_grid);
+        int64_t grid = workgroups > 0 ? workgroups
+                                      : (use_lds ? s->lds_grid
+                                         : (variant == 4 || variant == 6) ? s->persistent_w2_grid
+                                                                          : s->persistent_grid);
         const int64_t useful = (n_rays + tpb - 1) / tpb;   // never more workgroups than rays / tpb
         if (grid > useful) grid = useful;
         if (use_lds) {
@@ -930,6 +1014,23 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
             A.lds.ncy = s->lds.ncy;
             hipLaunchKernelGGL(trace_persistent_lds_kernel, dim3((unsigned)grid), dim3(768), (unsigned)s->lds_bytes,
                                st, A, ctr, 64);
+        } else if (variant >= 4) {
+            LocatorT<uint32_t> l32;
+            l32.cells = s->d_cells32;
+            l32.verts = A.loc.verts;
+            l32.poly_off = A.loc.poly_off;
+            l32.row_off = A.loc.row_off;
+            l32.row_edges = A.loc.row_edges;
+            l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
+            if (variant == 4)
+                hipLaunchKernelGGL((trace_persistent_g_kernel<uint64_t, 2>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   A.loc, ctr, 64);
+            else if (variant == 5)
+                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   l32, ctr, 64);
+            else
+                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 2>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   l32, ctr, 64);
         } else {
             hipLaunchKernelGGL(trace_persistent_kernel, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
         }
@@ -938,11 +1039,33 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
     return WGRT_OK;
 }
 
+wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays,
+                                    int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
+                                    wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
+                                    int variant, int workgroups) {
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
+                        variant, workgroups, false);
+}
+
 wgrt_status wgrt_trace_fullcolor(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays,
                                  int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream) {
-    return wgrt_trace_fullcolor_ex(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats,
-                                   per_ray_bounces, stream, 0, 0);
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, 0, 0,
+                        false);
+}
+
+wgrt_status wgrt_trace_single_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                                 uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                                 uint32_t *per_ray_bounces, void *stream, int variant, int workgroups) {
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
+                        variant, workgroups, true);
+}
+
+wgrt_status wgrt_trace_single(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                              uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                              uint32_t *per_ray_bounces, void *stream) {
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, 0, 0,
+                        true);
 }
 
 wgrt_status wgrt_scene_classify(const wgrt_scene *s, const double *xy, int64_t n, uint64_t *out_mask,
@@ -952,6 +1075,36 @@ wgrt_status wgrt_scene_classify(const wgrt_scene *s, const double *xy, int64_t n
     const int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(classify_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        make_locator(s), s->npoly, xy, n, out_mask);
+    HIP_TRY(hipGetLastError());
+    return WGRT_OK;
+}
+
+wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t nx, int32_t ny,
+                           const int32_t *lambdas, int32_t n_lambdas, int64_t block_lo, int64_t block_hi,
+                           const wgrt_ray_columns *out, uint32_t *rng_states, void *stream) {
+    if (!out || !lambdas) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL columns / lambdas");
+    if (rays_per_fov < 1 || nx < 1 || ny < 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "sizes must be positive");
+    if (n_lambdas < 1 || n_lambdas > 8) return fail(WGRT_ERR_INVALID_ARGUMENT, "1..8 wavelengths");
+    const int64_t nblk = (int64_t)nx * ny * n_lambdas;
+    if (block_lo < 0 || block_lo > block_hi || block_hi > nblk)
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "block range outside [0, nx * ny * n_lambdas]");
+    if (rays_per_fov >= 2 && !points) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL points");
+    RayInitArgs A{};
+    A.points = points;
+    float *const cols[12] = {out->x, out->y, out->gap_x, out->gap_y, out->pol, out->azi, out->m, out->n,
+                             out->lmd_num, out->te, out->tm, out->delta_phase};
+    for (int c = 0; c < 12; ++c) A.col[c] = cols[c];
+    A.rng = rng_states;
+    A.n = (block_hi - block_lo) * rays_per_fov;
+    A.R = rays_per_fov;
+    A.blk_lo = block_lo;
+    A.gid_offset = block_lo * rays_per_fov;
+    A.ny = ny;
+    A.nl = n_lambdas;
+    for (int k = 0; k < n_lambdas; ++k) A.lambdas[k] = (float)lambdas[k];
+    if (A.n == 0) return WGRT_OK;
+    const int64_t blocks = std::min<int64_t>((A.n + 255) / 256, 65536);
+    hipLaunchKernelGGL(rays_init_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }

@@ -58,6 +58,28 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
     accepted too.  stats: optional int64[4] device tensor that is added to
     (bounces, bad_rays, eyebox_hits, reserved).
     """
+    if scene.single_lambda:
+        raise ValueError("trace_fullcolor needs a full-colour scene; use trace_single for a single-wavelength one")
+    _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
+           workgroups, single=False)
+
+
+def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
+                 gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
+                 per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
+                 workgroups: int = 0) -> None:
+    """One launch of the single-wavelength kernel (``process_rays_kernel_pro``, GRTF:419-831)
+    through ``wgrt_trace_single_ex``: no ``lmd_num`` column (ignored if present),
+    matrix_EB [NY, NX, 80, 120], branch guard ener * efficiency > 1e-15.  The scene must be
+    a single-wavelength one (``Scene.from_geometry(..., wavelength=l)`` or 3-D LUTs)."""
+    if not scene.single_lambda:
+        raise ValueError("trace_single needs a single-wavelength scene (Scene.from_geometry(..., wavelength=l))")
+    _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
+           workgroups, single=True)
+
+
+def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
+           workgroups, single):
     device = torch.device("cuda", scene.device)
     x = rays["x"]
     N = x.numel() if n_rays is None else int(n_rays)
@@ -65,6 +87,8 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
         raise ValueError(f"n_rays={N} out of range for {x.numel()} rays")
     cols = {}
     for k in READ_COLUMNS:
+        if single and k == "lmd_num":
+            continue
         if k not in rays:
             raise ValueError(f"missing ray column {k!r}")
         cols[k] = _as_dev(rays[k], torch.float32, k, device, x.numel())
@@ -80,16 +104,52 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
         if per_ray_bounces.dtype not in (torch.int32, torch.uint32):
             raise TypeError("per_ray_bounces must be uint32 / int32")
         _as_dev(per_ray_bounces, per_ray_bounces.dtype, "per_ray_bounces", device, x.numel())
-    r = Rays(**{k: ctypes.c_void_p(cols[k].data_ptr()) for k in READ_COLUMNS})
+    r = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in cols.items()})
     for k in ("gap_x", "gap_y", "pol", "azi"):
         setattr(r, k, ctypes.c_void_p(rays[k].data_ptr()) if k in rays else None)
-    check(load().wgrt_trace_fullcolor_ex(
+    fn = load().wgrt_trace_single_ex if single else load().wgrt_trace_fullcolor_ex
+    check(fn(
         scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
         ctypes.c_void_p(matrix_EB.data_ptr()),
         ctypes.c_void_p(stats.data_ptr()) if stats is not None else None,
         ctypes.c_void_p(per_ray_bounces.data_ptr()) if per_ray_bounces is not None else None,
         ctypes.c_void_p(_stream_handle(device, stream)), int(variant), int(workgroups)),
-        "wgrt_trace_fullcolor")
+        "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
+
+
+def init_rays(points, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int, blocks=None,
+              device="cuda", all_columns: bool = True, stream=None):
+    """Build a ray batch on the device (``wgrt_rays_init``; replaces MAIN:59-115 and the RNG
+    seeding at MAIN:158, bit-identical to ``rays.build_rays`` + ``rays.rng_seeds``).
+
+    ``points``: the R/2 origins (numpy or torch float64 [R/2, 2]); ``blocks=(lo, hi)``
+    builds FoV x wavelength blocks [lo, hi) only (one rank's shard, global ids from lo * R).
+    ``all_columns=False`` allocates only the eight columns the kernel reads.
+    Returns ``(rays, rng_states)``: a dict of float32 tensors and an int32 view of the
+    uint32 RNG states."""
+    device = torch.device(device)
+    if device.index is None:
+        device = torch.device("cuda", torch.cuda.current_device())
+    R = int(rays_per_fov)
+    lam = np.ascontiguousarray(list(lambdas), dtype=np.int32)
+    nblk = num_fov_x * num_fov_y * len(lam)
+    lo, hi = (0, nblk) if blocks is None else (int(blocks[0]), int(blocks[1]))
+    if not 0 <= lo <= hi <= nblk:
+        raise ValueError(f"block range {blocks} outside [0, {nblk}]")
+    pts = points if isinstance(points, torch.Tensor) else torch.from_numpy(np.asarray(points, dtype=np.float64))
+    pts = pts.to(device=device, dtype=torch.float64).contiguous()
+    if tuple(pts.shape) != (R // 2, 2):
+        raise ValueError(f"points must have shape ({R // 2}, 2), got {tuple(pts.shape)}")
+    N = (hi - lo) * R
+    names = RAY_COLUMNS if all_columns else READ_COLUMNS
+    rays = {k: torch.empty(N, dtype=torch.float32, device=device) for k in names}
+    rng = torch.empty(N, dtype=torch.int32, device=device)
+    cols = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in rays.items()})
+    check(load().wgrt_rays_init(ctypes.c_void_p(pts.data_ptr()), R, int(num_fov_x), int(num_fov_y),
+                                lam.ctypes.data_as(ctypes.c_void_p), len(lam), lo, hi, ctypes.byref(cols),
+                                ctypes.c_void_p(rng.data_ptr()), ctypes.c_void_p(_stream_handle(device, stream))),
+          "wgrt_rays_init")
+    return rays, rng
 
 
 def classify_points(scene: Scene, xy: torch.Tensor, stream=None) -> torch.Tensor:
@@ -114,5 +174,5 @@ def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor
     return out
 
 
-__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "rays_to_device", "classify_points",
+__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "rays_to_device", "classify_points",
            "selftest_math", "RAY_COLUMNS", "_lib"]

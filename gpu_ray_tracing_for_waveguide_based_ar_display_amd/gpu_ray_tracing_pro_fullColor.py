@@ -6,7 +6,8 @@ Same flow as the reference script, on the MI355X kernel:
 2. the seven RCWA LUTs -- the reference's ``.npy`` files when ``lut_dir`` is given
    (MAIN:28-34), otherwise the seeded synthetic set (the files are not available offline);
 3. ray batch: ``num_rays_per_FoV / 2`` in-coupler origins shared by every FoV x wavelength
-   block, TE then TM halves (MAIN:59-115), RNG seeds ``0x9E3779B9 * (gid + 1)`` (MAIN:158);
+   block, TE then TM halves (MAIN:59-115), RNG seeds ``0x9E3779B9 * (gid + 1)`` (MAIN:158),
+   laid out on the device by ``wgrt_rays_init``;
 4. ``num_iter`` chained launches of the bounce kernel (MAIN:169-177), timed with HIP events
    (no JIT in the timed region, unlike the reference's wall clock);
 5. efficiencies ``A = sum(EB) / N / num_iter``, ``eff_c = 3 * sum(A[lambda])`` (MAIN:186-192)
@@ -34,9 +35,9 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
 
     from .couplers_coor import design_geometry
     from .distributed import make_shard, reduce_eyebox
-    from .engine import Scene, rays_to_device, trace_fullcolor
+    from .engine import Scene, init_rays, trace_fullcolor
     from .luts import load_luts, synthetic_luts, validate_luts
-    from .rays import build_rays, generate_points_in_polygon, rng_seeds
+    from .rays import generate_points_in_polygon
 
     world = dist.get_world_size() if dist.is_initialized() else 1
     rank = dist.get_rank() if dist.is_initialized() else 0
@@ -59,9 +60,10 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
         dist.broadcast(t, src=0)
         points = t.cpu().numpy()
     shard = make_shard(num_FOV_x, num_FOV_y, len(lambdas), R, world, rank)
-    host = build_rays(points, num_FOV_x, num_FOV_y, lambdas, R, blocks=(shard.block_lo, shard.block_hi))
-    rays = rays_to_device(host, dev)
-    rng = torch.from_numpy(rng_seeds(shard.n_rays, shard.gid_offset).view(np.int32)).to(dev)
+    # ray columns and RNG seeds built on the device (MAIN:59-158 without the host arrays:
+    # 48 B x N of host memory and its upload at the reference's 100 x 75 x 3 x 5000 default)
+    rays, rng = init_rays(points, num_FOV_x, num_FOV_y, lambdas, R, blocks=(shard.block_lo, shard.block_hi),
+                          device=dev, all_columns=False)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     stats = torch.zeros(4, dtype=torch.int64, device=dev)
     num_rays = num_FOV_x * num_FOV_y * len(lambdas) * R

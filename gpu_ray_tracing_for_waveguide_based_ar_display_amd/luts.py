@@ -59,6 +59,12 @@ PROFILES = {
     "deep": dict(ic=(0.40, 0.05), r0=(0.90, 0.03), r1=(0.03, 0.90),
                  fc_fold=(0.03, 0.10), fc_keep=0.985, fc_back=0.03, fc2_keep=0.955,
                  oc_turn=0.02, oc_out=(0.02, 0.06), oc_keep=0.985),
+    # Lossless, evenly split interactions: with shortened hops (tests scale lut_gap) rays
+    # live for 100+ bounces and ener = prod(e) falls below the single-wavelength kernel's
+    # 1e-15 guard (GRTF:444), which the other profiles practically never reach.
+    "balanced": dict(ic=(0.45, 0.45), r0=(0.5, 0.5), r1=(0.5, 0.5),
+                     fc_fold=(0.5, 0.5), fc_keep=1.0, fc_back=0.5, fc2_keep=1.0,
+                     oc_turn=0.33, oc_out=(0.33, 0.33), oc_keep=1.0),
 }
 
 
@@ -181,3 +187,15 @@ def load_luts(directory: str = ".", suffix: str = "_fullColor.npy") -> dict:
         path = os.path.join(directory, name + suffix)
         luts[name] = np.load(path, allow_pickle=False)
     return luts
+
+
+def single_wavelength(luts: dict, lut_TIR: np.ndarray, lut_gap: np.ndarray, l: int):
+    """Wavelength ``l`` of a full-colour set, in the single-wavelength kernel's shapes
+    (process_rays_kernel_pro, GRTF:419-427): lut_ic* / lut_TIR / lut_gap [NX, NY, C],
+    lut_fc* / lut_oc* [n_slices, NX, NY, C].  Returns ``(luts, lut_TIR, lut_gap)``."""
+    out = {}
+    for k in ("lut_ic1", "lut_ic2", "lut_ic3"):
+        out[k] = np.ascontiguousarray(luts[k][l])
+    for k in ("lut_fc1", "lut_fc2", "lut_oc1", "lut_oc2"):
+        out[k] = np.ascontiguousarray(luts[k][:, l])
+    return out, np.ascontiguousarray(lut_TIR[l]), np.ascontiguousarray(lut_gap[l])

@@ -79,14 +79,16 @@ def build_rays(points: np.ndarray, num_fov_x: int, num_fov_y: int, lambdas, rays
     per_ray = lambda v: np.repeat(v.reshape(-1)[lo:hi], R)
     r = np.arange(N) % R
     te_half = r < half
-    origin = np.tile(np.concatenate([pts, pts]).astype(np.float32), (nblk, 1))
+    used = r < 2 * half   # odd R: MAIN's halves cover 2 * floor(R / 2) rays, the last stays all-zero
+    block_pts = np.concatenate([pts, pts, np.zeros((R - 2 * half, 2))]).astype(np.float32)
+    origin = np.tile(block_pts, (nblk, 1))
     zeros = np.zeros(N, dtype=np.float32)
+    z = lambda v: np.where(used, v, np.float32(0)).astype(np.float32)
     return {
         "x": np.ascontiguousarray(origin[:, 0]),
         "y": np.ascontiguousarray(origin[:, 1]),
         "gap_x": zeros.copy(), "gap_y": zeros.copy(), "pol": zeros.copy(), "azi": zeros.copy(),
-        "m": per_ray(ii).astype(np.float32), "n": per_ray(jj).astype(np.float32),
-        "lmd_num": per_ray(ll).astype(np.float32),
-        "te": te_half.astype(np.float32), "tm": (~te_half).astype(np.float32),
+        "m": z(per_ray(ii)), "n": z(per_ray(jj)), "lmd_num": z(per_ray(ll)),
+        "te": te_half.astype(np.float32), "tm": (used & ~te_half).astype(np.float32),
         "delta_phase": zeros.copy(),
     }

@@ -84,6 +84,11 @@ typedef struct {
     const float *x, *y, *gap_x, *gap_y, *pol, *azi, *m, *n, *lmd_num, *te, *tm, *delta_phase;
 } wgrt_rays;
 
+/* The same twelve columns as outputs (wgrt_rays_init). */
+typedef struct {
+    float *x, *y, *gap_x, *gap_y, *pol, *azi, *m, *n, *lmd_num, *te, *tm, *delta_phase;
+} wgrt_ray_columns;
+
 typedef struct {
     uint64_t bounces;      /* ray-bounce events: 1 in-coupling + loop iterations, per ray */
     uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num               */
@@ -131,6 +136,36 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *ra
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
                                     int variant, int workgroups);
+
+/* One launch of the single-wavelength bounce kernel process_rays_kernel_pro
+ * (reference GPU_ray_tracing_functions.py:419-831): the 32-argument form without the
+ * lmd_num column, LUTs [nx, ny, ch] / [n_slices, nx, ny, ch] (a wgrt_scene_desc with
+ * num_lmd = 1 has exactly that memory layout), matrix_EB [ny, nx, 80, 120], and the
+ * R2..R5 branch guard ener * efficiency > 1e-15 (GRTF:444) instead of > 0.
+ * rays->lmd_num is ignored and may be NULL.  WGRT_ERR_INVALID_ARGUMENT if the scene has
+ * num_lmd != 1.  Everything else as wgrt_trace_fullcolor / _ex. */
+wgrt_status wgrt_trace_single(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                              uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                              uint32_t *per_ray_bounces, void *stream);
+wgrt_status wgrt_trace_single_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
+                                 int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
+                                 wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream, int variant,
+                                 int workgroups);
+
+/* Device-side ray setup (replaces the host loop MAIN:59-115 and the seeding at MAIN:158):
+ * fills FoV x wavelength blocks [block_lo, block_hi) of the batch -- block b =
+ * (ii * ny + jj) * n_lambdas + k, rays [b * R, (b + 1) * R) -- into DEVICE columns of
+ * (block_hi - block_lo) * R floats, i.e. one rank's shard at local index 0:
+ *   x, y = points[r] (first R/2 rays, TE: te 1, tm 0) / points[r - R/2] (TM: te 0, tm 1),
+ *   m = ii, n = jj, lmd_num = lambdas[k] (HOST int32[n_lambdas], n_lambdas <= 8;
+ *   MAIN uses 0..2), gap_x = gap_y = pol = azi = delta_phase = 0.
+ * points: DEVICE float64 [R / 2, 2] (generate_points_in_polygon, GRTF:12-23), rounded to
+ * float32 as numpy assignment does.  Odd R: the last ray of each block is all-zero, as in
+ * MAIN.  rng_states (optional, DEVICE uint32) = 0x9E3779B9 * (gid + 1) with global gid =
+ * block_lo * R + i.  Any column may be NULL (not written).  Asynchronous on stream. */
+wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t nx, int32_t ny,
+                           const int32_t *lambdas, int32_t n_lambdas, int64_t block_lo, int64_t block_hi,
+                           const wgrt_ray_columns *out, uint32_t *rng_states, void *stream);
 
 /* Polygon membership of n points (DEVICE xy[n, 2]) through the scene's locator:
  * bit k of out_mask[i] = is_inside_or_on_edge(point i, polygon k) with polygon order

@@ -1,8 +1,9 @@
 """TEST INFRASTRUCTURE ONLY -- the CPU parity oracle.
 
-``oracle/wgrt_oracle.c`` restates the reference kernel
-``process_rays_kernel_pro_fullColor`` (GPU_ray_tracing_functions.py:833-1246)
-in plain float64 C; this module loads it with ctypes.  Only ``tests/``,
+``oracle/wgrt_oracle.c`` restates the reference kernels
+``process_rays_kernel_pro_fullColor`` (GPU_ray_tracing_functions.py:833-1246) and
+``process_rays_kernel_pro`` (GPU_ray_tracing_functions.py:419-831, the same FSM without
+the wavelength axis and with threshold 1e-15) in plain float64 C; this module loads it with ctypes.  Only ``tests/``,
 ``__graft_entry__.smoke()`` and ``bench.py``'s ``cpu_baseline`` leg may import
 it -- as the checker / the timed CPU baseline, never as a product path.
 
@@ -39,7 +40,7 @@ class _Scene(ctypes.Structure):
         ("fc1", _f64p), ("fc2", _f64p), ("oc1", _f64p), ("oc2", _f64p),
         ("num_lmd", ctypes.c_int32), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
         ("ch5", ctypes.c_int32), ("ch3", ctypes.c_int32),
-        ("n_g", ctypes.c_double),
+        ("n_g", ctypes.c_double), ("threshold", ctypes.c_double),
     ]
 
 
@@ -103,6 +104,15 @@ class OracleScene:
     def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
                  eff_reg_FOV_range, luts: dict, lut_TIR, lut_gap):
         c = lambda a, dt=np.float64: np.ascontiguousarray(a, dtype=dt)
+        # single-wavelength LUT shapes (GRTF:419-427): lut_TIR [NX, NY, 4], ... -> lambda axis of 1
+        self.single_lambda = np.ndim(lut_TIR) == 3
+        if self.single_lambda:
+            luts = dict(luts)
+            for name in ("lut_ic1", "lut_ic2", "lut_ic3"):
+                luts[name] = np.asarray(luts[name])[None]
+            for name in ("lut_fc1", "lut_fc2", "lut_oc1", "lut_oc2"):
+                luts[name] = np.asarray(luts[name])[:, None]
+            lut_TIR, lut_gap = np.asarray(lut_TIR)[None], np.asarray(lut_gap)[None]
         self._keep = dict(
             IC=c(IC), FC=c(FC), FC_offset=c(FC_offset, np.int64), OC=c(OC), OC_offset=c(OC_offset, np.int64),
             eff1=c(eff_reg1), eff2=c(eff_reg2), fov=c(eff_reg_FOV), rng=c(eff_reg_FOV_range),
@@ -120,15 +130,23 @@ class OracleScene:
             _p(k["fov"], _f64p), _p(k["rng"], _f64p), _p(k["tir"], _f64p), _p(k["gap"], _f64p),
             *[k[n].ctypes.data_as(_f64p) for n in ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1",
                                                    "lut_fc2", "lut_oc1", "lut_oc2")],
-            L, NX, NY, k["lut_ic1"].shape[-1], k["lut_fc1"].shape[-1], float(n_g))
+            L, NX, NY, k["lut_ic1"].shape[-1], k["lut_fc1"].shape[-1], float(n_g),
+            1e-15 if self.single_lambda else 0.0)
 
     @classmethod
-    def from_geometry(cls, geom, luts):
+    def from_geometry(cls, geom, luts, wavelength: int | None = None):
+        """``wavelength=l``: the single-wavelength scene of wavelength l (process_rays_kernel_pro)."""
+        tir, gap = geom.lut_TIR, geom.lut_gap
+        if wavelength is not None:
+            luts = {k: (v[wavelength] if k in ("lut_ic1", "lut_ic2", "lut_ic3") else v[:, wavelength])
+                    for k, v in luts.items() if k.startswith("lut_")}
+            tir, gap = tir[wavelength], gap[wavelength]
         return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
-                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts, geom.lut_TIR,
-                   geom.lut_gap)
+                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts, tir, gap)
 
     def eb_shape(self):
+        if self.single_lambda:
+            return (self.ny, self.nx, 80, 120)
         return (self.num_lmd, self.ny, self.nx, 80, 120)
 
     def trace(self, rays: dict, rng: np.ndarray, eb: np.ndarray, gid_offset: int = 0,
@@ -139,11 +157,12 @@ class OracleScene:
         when ``fate`` is set."""
         cols = {k: np.ascontiguousarray(rays[src], dtype=np.float32) for k, src in
                 (("x", "x"), ("y", "y"), ("m", "m"), ("n", "n"), ("lmd", "lmd_num"), ("te", "te"),
-                 ("tm", "tm"), ("dph", "delta_phase"))}
+                 ("tm", "tm"), ("dph", "delta_phase")) if not (self.single_lambda and k == "lmd")}
         N = cols["x"].shape[0]
         assert rng.dtype == np.uint32 and rng.flags.c_contiguous and rng.shape == (N,)
         assert eb.dtype == np.float32 and eb.flags.c_contiguous and eb.shape == self.eb_shape()
-        r = _Rays(*[_p(cols[k], _f32p) for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")])
+        r = _Rays(*[_p(cols[k], _f32p) if k in cols else None
+                    for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")])
         counts = np.zeros(N, dtype=np.uint32) if per_ray_bounces else None
         fates = np.zeros(N, dtype=np.uint8) if fate else None
         tot = lib().wgrt_oracle_trace(ctypes.byref(self._s), ctypes.byref(r), N, int(gid_offset),

@@ -189,7 +189,7 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
     ray_state st;
     st.x = (double)rays->x[i];
     st.y = (double)rays->y[i];
-    int m = (int)rays->m[i], n = (int)rays->n[i], l = (int)rays->lmd[i];
+    int m = (int)rays->m[i], n = (int)rays->n[i], l = rays->lmd ? (int)rays->lmd[i] : 0;
     st.Ete = (double)rays->te[i];
     st.Etm = (double)rays->tm[i];
     st.dph = (double)rays->dph[i];
@@ -290,11 +290,11 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e2 = (E2.te * E2.te + E2.tm * E2.tm) * cos(th2) / st.cos_th;
                 double en1 = st.ener * e1, en2 = st.ener * e2;
                 double u = rng_draw(&s, gid);
-                if (u <= e1 && en1 > 0.0) {
+                if (u <= e1 && en1 > sc->threshold) {
                     take(&st, &E1, th1, tir[0], gap + 0);
                     st.ener = en1 * 1.0;
                     region = 2;
-                } else if (u <= e1 + e2 && en2 > 0.0) {
+                } else if (u <= e1 + e2 && en2 > sc->threshold) {
                     take(&st, &E2, th2, tir[1], gap + 2);
                     st.ener = en2 * 1.0;
                     region = 3;
@@ -348,15 +348,15 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e3 = (E3.te * E3.te + E3.tm * E3.tm) * cos(th_ic1) / st.cos_th / n_g;
                 double en1 = st.ener * e1, en2 = st.ener * e2, en3 = st.ener * e3;
                 double u = rng_draw(&s, gid);
-                if (u <= e1 && en1 > 0.0) {
+                if (u <= e1 && en1 > sc->threshold) {
                     take(&st, &E1, th1, tir[1], gap + 2);
                     st.ener = en1 * 1.0;
                     region = 4;
-                } else if (u <= e1 + e2 && en2 > 0.0) {
+                } else if (u <= e1 + e2 && en2 > sc->threshold) {
                     take(&st, &E2, th2, tir[3], gap + 6);
                     st.ener = en2 * 1.0;
                     region = 5;
-                } else if (u <= e1 + e2 + e3 && en3 > 0.0) {
+                } else if (u <= e1 + e2 + e3 && en3 > sc->threshold) {
                     const double *rect = sc->eff_reg_fov + 8 * ((int64_t)m * sc->ny + n);
                     if (inside_or_on_edge(st.x, st.y, rect, 4)) { eb_add(sc, eb, l, m, n, st.x, st.y); why = (uint8_t)(10 * region + 3); }
                     else why = (uint8_t)(10 * region + 4);

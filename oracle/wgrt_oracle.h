@@ -1,5 +1,6 @@
 /* wgrt_oracle.h -- TEST INFRASTRUCTURE ONLY: CPU float64 restatement of the reference's
- * process_rays_kernel_pro_fullColor (GPU_ray_tracing_functions.py:833-1246).
+ * process_rays_kernel_pro_fullColor (GPU_ray_tracing_functions.py:833-1246) and, with
+ * lmd == NULL and threshold 1e-15, process_rays_kernel_pro (GPU_ray_tracing_functions.py:419-831).
  * Parity pinned by the golden fixtures under tests/golden.  Never linked into the product library. */
 #ifndef WGRT_ORACLE_H
 #define WGRT_ORACLE_H
@@ -24,10 +25,12 @@ typedef struct {
     const double *oc1, *oc2;          /* [nOC, L, NX, NY, ch5] */
     int32_t num_lmd, nx, ny, ch5, ch3;
     double n_g;
+    double threshold;   /* R2..R5 guard ener * eff > threshold: 0 full colour (GRTF:859),
+                           1e-15 single wavelength (GRTF:444) */
 } wgrt_oracle_scene;
 
 typedef struct {
-    const float *x, *y, *m, *n, *lmd, *te, *tm, *dph;
+    const float *x, *y, *m, *n, *lmd, *te, *tm, *dph;   /* lmd NULL: single wavelength, l = 0 */
 } wgrt_oracle_rays;
 
 /* Traces rays [0, n_rays) of the given shard (global ids gid_offset + i); updates rng

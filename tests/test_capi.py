@@ -84,3 +84,24 @@ def test_scene_create_validates_before_gpu(lib, field, value, msg):
 def test_trace_rejects_null_scene(lib):
     r = _lib.Rays()
     assert lib.wgrt_trace_fullcolor(None, ctypes.byref(r), 10, 0, None, None, None, None, None) == 1
+    assert lib.wgrt_trace_single(None, ctypes.byref(r), 10, 0, None, None, None, None, None) == 1
+    assert lib.wgrt_trace_single_ex(None, ctypes.byref(r), 10, 0, None, None, None, None, None, 0, 0) == 1
+
+
+def test_single_wavelength_desc_matches_full_colour_slice():
+    """Single-wavelength LUT shapes (process_rays_kernel_pro, GRTF:419-427) are described as a
+    one-wavelength scene whose memory is exactly that wavelength's slice of the full set."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import single_wavelength, synthetic_luts
+    g = design_geometry(4, 3)
+    L = synthetic_luts(g, seed=1)
+    S, tir, gap = single_wavelength(L, g.lut_TIR, g.lut_gap, 2)
+    assert S["lut_ic1"].shape == (4, 3, 42) and S["lut_fc1"].shape == (g.num_fc_slices, 4, 3, 26)
+    assert tir.shape == (4, 3, 4) and gap.shape == (4, 3, 8)
+    args = (g.IC, g.FC, g.FC_offset, g.OC, g.OC_offset, g.n_g, g.eff_reg1, g.eff_reg2, g.eff_reg_FOV,
+            g.eff_reg_FOV_range)
+    d, keep, dims = _lib.make_desc(*args, S["lut_ic1"], S["lut_ic2"], S["lut_ic3"], S["lut_fc1"], S["lut_fc2"],
+                                   S["lut_oc1"], S["lut_oc2"], tir, gap)
+    assert dims == (1, 4, 3, g.num_fc_slices, g.num_oc_slices)
+    np.testing.assert_array_equal(keep["fc1"][:, 0], L["lut_fc1"][:, 2])
+    np.testing.assert_array_equal(keep["tir"][0], g.lut_TIR[2])

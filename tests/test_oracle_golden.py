@@ -1,7 +1,8 @@
 """Pin the CPU oracle (oracle/wgrt_oracle.c) to the reference's own kernel outputs.
 
 The fixtures were produced by running GPU_ray_tracing_functions.py:833-1246
-unmodified (tests/golden/gen_golden.py).  Bar: bit-exact rng_states,
+(full colour) and :419-831 (single wavelength, ``s*`` cases) unmodified
+(tests/golden/gen_golden.py).  Bar: bit-exact rng_states,
 matrix_EB and per-ray bounce counts after 1 and after 4 launches.
 """
 import numpy as np
@@ -22,7 +23,7 @@ def test_inputs_regenerate_bit_identically(case):
 
 @pytest.mark.parametrize("threads", [1, 4])
 def test_oracle_matches_reference(case, threads):
-    sc = OracleScene.from_geometry(case.geom, case.luts)
+    sc = OracleScene.from_geometry(case.geom, case.luts, wavelength=case.wavelength)
     rng = case.fresh_rng()
     eb = np.zeros(case.eb_shape(), np.float32)
     num_iter = int(case.f["num_iter"])
@@ -39,7 +40,7 @@ def test_oracle_matches_reference(case, threads):
 
 def test_oracle_sharding_invariance(case):
     """Tracing R-aligned gid ranges separately (with gid_offset) equals one pass."""
-    sc = OracleScene.from_geometry(case.geom, case.luts)
+    sc = OracleScene.from_geometry(case.geom, case.luts, wavelength=case.wavelength)
     rng_full = case.fresh_rng()
     eb_full = np.zeros(case.eb_shape(), np.float32)
     sc.trace(case.rays, rng_full, eb_full)
@@ -53,3 +54,16 @@ def test_oracle_sharding_invariance(case):
         rng_sh[a:b] = r
     np.testing.assert_array_equal(rng_sh, rng_full)
     np.testing.assert_array_equal(eb_sh, eb_full)
+
+
+def test_single_wavelength_threshold_is_pinned():
+    """s5_thr_532 reaches the 1e-15 energy guard of process_rays_kernel_pro (GRTF:444):
+    the same trace with the full-colour kernel's guard (0, GRTF:859) must differ, so the
+    fixture really pins the threshold."""
+    case = GoldenCase("s5_thr_532")
+    sc = OracleScene.from_geometry(case.geom, case.luts, wavelength=case.wavelength)
+    sc._s.threshold = 0.0
+    rng = case.fresh_rng()
+    eb = np.zeros(case.eb_shape(), np.float32)
+    _, per_ray = sc.trace(case.rays, rng, eb, per_ray_bounces=True)
+    assert (per_ray != case.f["bounces"][0]).sum() > 10
