@@ -45,7 +45,7 @@ def parse():
     ap.add_argument("--lambdas", default="0,1,2")
     ap.add_argument("--lut-profile", default="default")
     ap.add_argument("--lut-seed", type=int, default=0)
-    ap.add_argument("--variant", type=int, default=0, help="0 auto, 1 grid, 2 persistent")
+    ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
     ap.add_argument("--workgroups", type=int, default=0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
@@ -172,7 +172,13 @@ def main():
 
 
 def kernel_name(variant, scene):
-    return {1: "trace_grid_kernel", 3: "trace_persistent_lds_kernel"}.get(variant, "trace_persistent_kernel")
+    """Name of the kernel a launch runs (wgrt_trace_fullcolor_ex's variant table; auto = 5
+    when the scene has <= 16 polygons, else 2)."""
+    if variant == 0:
+        variant = 5 if scene.info()["n_polygons"] <= 16 else 2
+    return {1: "trace_grid_kernel", 2: "trace_persistent_kernel", 3: "trace_persistent_lds_kernel",
+            4: "trace_persistent_g_kernel<unsigned long, 4>", 5: "trace_persistent_g_kernel<unsigned int, 3>",
+            6: "trace_persistent_g_kernel<unsigned int, 4>"}[variant]
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):

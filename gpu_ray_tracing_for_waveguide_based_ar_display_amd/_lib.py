@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG, "libwgrt.so")
 
 ABI_VERSION = 1
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
-            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
+            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -56,6 +56,11 @@ class Rays(ctypes.Structure):
 class TraceStats(ctypes.Structure):
     _fields_ = [("bounces", ctypes.c_uint64), ("bad_rays", ctypes.c_uint64),
                 ("eyebox_hits", ctypes.c_uint64), ("reserved", ctypes.c_uint64)]
+
+
+class LaunchOpts(ctypes.Structure):
+    _fields_ = [("kernel", ctypes.c_int), ("variant", ctypes.c_int), ("workgroups", ctypes.c_int),
+                ("chunk_order", ctypes.c_void_p), ("n_chunk_order", ctypes.c_int64)]
 
 
 class SceneInfo(ctypes.Structure):
@@ -98,6 +103,9 @@ def load(path: str = LIB_PATH):
     L.wgrt_trace_single.argtypes = L.wgrt_trace_fullcolor.argtypes
     L.wgrt_trace_single_ex.restype = st
     L.wgrt_trace_single_ex.argtypes = L.wgrt_trace_fullcolor_ex.argtypes
+    L.wgrt_trace_opts.restype = st
+    L.wgrt_trace_opts.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, _vp, _vp, _vp, _vp,
+                                  _vp, ctypes.POINTER(LaunchOpts)]
     L.wgrt_rays_init.restype = st
     L.wgrt_rays_init.argtypes = [_vp, ctypes.c_int64, ctypes.c_int32, ctypes.c_int32, _vp, ctypes.c_int32,
                                  ctypes.c_int64, ctypes.c_int64, ctypes.POINTER(Rays), _vp, _vp]

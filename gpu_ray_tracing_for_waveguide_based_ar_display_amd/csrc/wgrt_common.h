@@ -46,7 +46,9 @@ constexpr int kTileGap = 4;       // lut_gap[8]
 constexpr int kTileEbRange = 12;  // eff_reg_FOV_range[m, n, 4]
 constexpr int kTileEbRect = 16;   // eff_reg_FOV[m, n, 4, 2]
 constexpr int kTileCosIc1 = 24;   // cos(lut_ic1[l, m, n, 0].real)
-constexpr int kTileHeader = 28;
+constexpr int kTileTirRot = 28;   // (cos, sin) of lut_TIR[k], k = 0..3: the phase step of a taken branch
+constexpr int kTileHopRot = 36;   // (cos, sin) of 2 * lut_TIR[k], k = 0, 1: the phase step of a miss hop
+constexpr int kTileHeader = 40;
 constexpr int kBlock = 28;        // cosA[3], pad, rec[3][8]
 constexpr int kBlockCos = 0;
 constexpr int kBlockRec = 4;

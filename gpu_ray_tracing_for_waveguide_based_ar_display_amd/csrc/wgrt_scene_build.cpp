@@ -241,7 +241,15 @@ void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles) {
             for (int64_t n = 0; n < NY; ++n) {
                 double *T = tiles.data() + (size_t)((l * NX + m) * NY + n) * TD;
                 const int64_t g = (l * NX + m) * NY + n;
-                for (int k = 0; k < 4; ++k) T[kTileTir + k] = d.lut_TIR[4 * g + k];
+                for (int k = 0; k < 4; ++k) {
+                    T[kTileTir + k] = d.lut_TIR[4 * g + k];
+                    T[kTileTirRot + 2 * k] = std::cos(d.lut_TIR[4 * g + k]);
+                    T[kTileTirRot + 2 * k + 1] = std::sin(d.lut_TIR[4 * g + k]);
+                }
+                for (int k = 0; k < 2; ++k) {
+                    T[kTileHopRot + 2 * k] = std::cos(2 * d.lut_TIR[4 * g + k]);
+                    T[kTileHopRot + 2 * k + 1] = std::sin(2 * d.lut_TIR[4 * g + k]);
+                }
                 for (int k = 0; k < 8; ++k) T[kTileGap + k] = d.lut_gap[8 * g + k];
                 const int64_t f = m * NY + n;
                 for (int k = 0; k < 4; ++k) T[kTileEbRange + k] = d.eff_reg_FOV_range[4 * f + k];
@@ -378,6 +386,9 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) 
     build_locator(polys, nv, cell_mm, out.loc);
     build_lds_image(polys, nv, 2 * cell_mm, kLdsBudget, out.lds);
     pack_tiles(d, out.tiles);
+    // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would
+    // make the reference's efficiencies NaN); such LUTs are rejected instead.
+    for (const double v : out.tiles) check(std::isfinite(v), "non-finite value in the LUTs / lut_TIR / lut_gap / eyebox tables");
     out.tile_doubles = tile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
 }
 

@@ -110,6 +110,7 @@ struct TraceArgs {
     int tile_d, nfc, noc, nx, ny, nl;
     double n_g, inv_n_g;
     double threshold;   // ener * efficiency > threshold guard of R2..R5: 0 full colour, 1e-15 single lambda
+    const int32_t *order;   // persistent variants: issue order of the 64-ray chunks (NULL: ascending)
     int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
 };
 
@@ -118,10 +119,17 @@ constexpr int kPolyEff2 = 1;
 constexpr int kPolyIC = 2;
 constexpr int kPolyFC0 = 3;
 
+#if defined(WGRT_DIAG) || defined(WGRT_TIMERS)
+// Diagnostic builds only.  Per-phase shader-clock cycles summed over lanes (grid kernel,
+// WGRT_TIMERS, tools/diag_timers.py): 0 interact: tile + sincos + branch fields, 1 decision,
+// 2 take / eyebox, 3 advance, 4 #interactions, 5 #advance calls.
+__device__ unsigned long long g_diag_tm[8];
+#endif
 #ifdef WGRT_DIAG
 // Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
 __device__ unsigned long long g_diag[16];
 __device__ unsigned long long g_diag_fallback;
+
 // region r: g_diag[6 + r] += number of wave executions, g_diag_act[r] += active lanes
 __device__ unsigned long long g_diag_act[16];
 __device__ __forceinline__ void diag_region(int r) {
@@ -204,30 +212,53 @@ __device__ __forceinline__ Field efield(double Ete, double Etm, double cd, doubl
     return Field{a_re + b_re, a_im + b_im, c_re + d_re, c_im + d_im};
 }
 
-// Output phase difference of E_field_cal: wrap(atan2(Etm') - atan2(Ete')), 0 phase for a
-// component with |.| < 1e-20 (GRTF:147-150).
-// The two atan2 run as two trips of one non-unrolled loop: one copy of the (register-hungry)
-// f64 atan2 body instead of two interleaved ones keeps the kernel's VGPR peak down.
-__device__ __forceinline__ double efield_phase(const Field &f, double te, double tm) {
-    double ph[2] = {0.0, 0.0};
-#pragma unroll 1
-    for (int k = 0; k < 2; ++k) {
-        const double y = k == 0 ? f.te_im : f.tm_im;
-        const double x = k == 0 ? f.te_re : f.tm_re;
-        const double mag = k == 0 ? te : tm;
-#ifdef WGRT_ABL_ATAN2
-        const double a = (mag >= 1e-20) ? y * x : 0.0;   // ablation build only
-#else
-        const double a = (mag >= 1e-20) ? atan2(y, x) : 0.0;
-#endif
-        if (k == 0) ph[0] = a;
-        else ph[1] = a;
-    }
-    return wrap_pi(ph[1] - ph[0]);
+// |Ete'|^2 + |Etm'|^2 of efield() without the "* 0.0" promotion terms: for finite inputs
+// (LUTs are checked at scene creation, ray state stays finite) those terms only change the
+// sign of zero components, so every component has the same magnitude as efield()'s and the
+// sum of squares is identical.  Used for the branch estimates only.
+__device__ __forceinline__ double efield_sq(double Ete, double Etm, double cd, double sd, const double *rec) {
+    const double pr = rec[0], pi = rec[1], qr = rec[2], qi = rec[3];
+    const double rr = rec[4], ri = rec[5], sr = rec[6], si = rec[7];
+    const double ti_re = cd * Etm, ti_im = sd * Etm;
+    const double a_re = pr * Ete + (rr * ti_re - ri * ti_im), a_im = pi * Ete + (rr * ti_im + ri * ti_re);
+    const double c_re = qr * Ete + (sr * ti_re - si * ti_im), c_im = qi * Ete + (sr * ti_im + si * ti_re);
+    return (a_re * a_re + a_im * a_im) + (c_re * c_re + c_im * c_im);
+}
+
+// The ray's phase difference delta_phase is carried as its phasor (cos, sin)(delta_phase),
+// which is all E_field_cal consumes (GRTF:135: phase = complex(cos(delta), sin(delta))).
+// E_field_cal's output phase wrap(atan2(Etm') - atan2(Ete')) (GRTF:145-150; 0 for a component
+// with |.| < 1e-20) becomes the unit phasor (Etm' / |Etm'|) * conj(Ete' / |Ete'|); adding
+// lut_TIR (a taken branch) or 2 * lut_TIR (a miss hop) becomes a multiplication by its
+// phasor.  The wrap is a no-op for a phasor.  The values equal the reference's cos / sin of
+// the accumulated phase up to last-ulp rounding -- the same order as the 1-ulp differences
+// between the device's and glibc's atan2 / sin / cos that any GPU evaluation of the
+// reference's formula has (tools/math_ulps.py: atan2 differs in 27 % of calls).  A
+// Monte-Carlo decision can change only if a uniform draw lands within ~1e-16 of a branch
+// threshold (about once per 1e8 launches of the C3 batch).
+struct Phasor {
+    double c, s;
+};
+
+__device__ __forceinline__ Phasor mul(const Phasor &a, const Phasor &b) {
+    return Phasor{a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c};
+}
+
+__device__ __forceinline__ Phasor field_phasor(const Field &f, double te, double tm) {
+    const bool ue = te >= 1e-20, um = tm >= 1e-20;
+    const double er = ue ? f.te_re : 1.0, ei = ue ? f.te_im : 0.0;
+    const double mr = um ? f.tm_re : 1.0, mi = um ? f.tm_im : 0.0;
+    const double den = (ue ? te : 1.0) * (um ? tm : 1.0);
+    // (mr + i mi) * (er - i ei) / (|Etm'| |Ete'|)
+    double inv = __builtin_amdgcn_rcp(den);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    return Phasor{(mr * er + mi * ei) * inv, (mi * er - mr * ei) * inv};
 }
 
 struct Ray {
-    double x, y, te, tm, dph, cos_t, ener;
+    double x, y, te, tm, cos_t, ener;
+    Phasor ph;   // (cos, sin) of delta_phase
     uint32_t s;
     int region;
 };
@@ -240,7 +271,17 @@ struct Lane {
     int l, m, n;
     uint32_t bounces;  // 1 in-coupling event + loop iterations (GRTF:905)
     bool hit;          // accumulated into matrix_EB
+#ifdef WGRT_TIMERS
+    uint64_t tm[6];
+#endif
 };
+#ifdef WGRT_TIMERS
+#define DIAG_CLK(v) const uint64_t v = __builtin_readcyclecounter()
+#define DIAG_ACC(k, a, b) (L.tm[k] += (b) - (a))
+#else
+#define DIAG_CLK(v) ((void)0)
+#define DIAG_ACC(k, a, b) ((void)0)
+#endif
 
 // Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
 // FoV / wavelength indices fall outside the scene.
@@ -265,17 +306,25 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
     L.r.y = (double)A.y[ld];
     L.r.te = (double)A.te[ld];
     L.r.tm = (double)A.tm[ld];
-    L.r.dph = (double)A.dph[ld];
+    {
+        double sd, cd;
+        sincos((double)A.dph[ld], &sd, &cd);
+        L.r.ph = Phasor{cd, sd};
+    }
     L.r.cos_t = 1.0;
     L.r.ener = 1.0;
     L.r.s = A.rng[ld];
     L.r.region = 0;
     L.bounces = 1;
     L.hit = false;
+#ifdef WGRT_TIMERS
+    for (int k = 0; k < 6; ++k) L.tm[k] = 0;
+#endif
     return true;
 }
 
 enum : int { kDie = -1, kTransit = -2 };
+constexpr int kChunk = 64;   // rays per work-queue chunk of the persistent variants
 
 
 
@@ -291,13 +340,10 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     const double *T = L.T;
     const double *B = T + kTileHeader + kBlock * blk;
     DIAG_REGION(0);   // interaction
+    DIAG_CLK(t0);
     double sd, cd;
-#ifdef WGRT_ABL_SINCOS
-    sd = r.dph * 0.5;   // ablation build only
-    cd = 1.0 - r.dph * 0.25;
-#else
-    sincos(r.dph, &sd, &cd);
-#endif
+    cd = r.ph.c;
+    sd = r.ph.s;
     const bool three = kind >= 3;
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
     const double denom = entry ? T[kTileCosIc1] : r.cos_t;
@@ -312,6 +358,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     // provably the reference's decision.  Otherwise -- about once in 1e12 draws -- the lane
     // recomputes every e_k exactly as the reference does.  The chosen branch's magnitudes
     // and efficiency are always computed exactly.
+#ifdef WGRT_EXP_OLD_EST   // experiment: the previous estimate code
     double q[3];
 #pragma unroll
     for (int k = 0; k < 3; ++k) {
@@ -322,6 +369,30 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         }
     }
     const double inv = 1.0 / denom;
+#else
+    // one branch at a time (a rolled loop keeps the register peak down)
+    double q[3] = {0.0, 0.0, 0.0};
+    const int nbr = three ? 3 : 2;
+#ifdef WGRT_EXP_UNROLL_SQ
+#pragma unroll
+    for (int k = 0; k < 3; ++k) {
+        if (k >= nbr) break;
+#else
+#pragma unroll 1
+    for (int k = 0; k < nbr; ++k) {
+#endif
+        const double v = efield_sq(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
+        q[0] = k == 0 ? v : q[0];
+        q[1] = k == 1 ? v : q[1];
+        q[2] = k == 2 ? v : q[2];
+    }
+    DIAG_CLK(t1);
+    DIAG_ACC(0, t0, t1);
+    // 1 / denom to ~1e-16 relative (estimates only): hardware reciprocal + two Newton steps
+    double inv = __builtin_amdgcn_rcp(denom);
+    inv = fma(inv, fma(-denom, inv, 1.0), inv);
+    inv = fma(inv, fma(-denom, inv, 1.0), inv);
+#endif
     double a0 = q[0] * B[0] * inv, a1 = q[1] * B[1] * inv;
     if (entry) {
         a0 *= A.n_g;
@@ -380,6 +451,16 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         else return kDie;
     }
 
+    DIAG_CLK(t2);
+    DIAG_ACC(1, t1, t2);
+#ifdef WGRT_TIMERS
+    L.tm[4] += 1;
+    struct Acc {
+        Lane &L;
+        uint64_t t;
+        __device__ ~Acc() { L.tm[2] += __builtin_readcyclecounter() - t; }
+    } acc_{L, t2};
+#endif
     if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
         DIAG_REGION(2);
         if (inside_or_on_edge(r.x, r.y, T + kTileEbRect, 4)) {
@@ -409,7 +490,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     if (entry) e = e * A.n_g;
     // take the branch (GRTF:872-882 and every branch body after it)
     const double norm = sqrt(cte * cte + ctm * ctm);
-    const double ph = efield_phase(f, cte, ctm);
+    const Phasor ph = field_phasor(f, cte, ctm);
     int tir, gap;
     if (kind == 0) { tir = b == 0 ? 0 : 2; gap = b == 0 ? 0 : 4; }
     else if (kind <= 2) { tir = b == 0 ? 0 : 1; gap = b == 0 ? 0 : 2; }
@@ -417,7 +498,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     r.cos_t = B[b];
     r.te = cte / norm;
     r.tm = ctm / norm;
-    r.dph = ph + T[kTileTir + tir];
+    r.ph = mul(ph, Phasor{T[kTileTirRot + 2 * tir], T[kTileTirRot + 2 * tir + 1]});
     r.x += T[kTileGap + gap];
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
@@ -442,9 +523,10 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     const double *T = L.T;
     // A miss hop's step is fixed by the region: R2 moves by gap[0:2] and adds 2*TIR[0],
     // R3 and R4 move by gap[2:4] and add 2*TIR[1] (R5 misses die).  Fetch it once.
+    // (kTileHopRot + g holds the phasor of 2*TIR[g / 2].)
     const int g = (r.region == 2) ? 0 : 2;
     const double gx = T[kTileGap + g], gy = T[kTileGap + g + 1];
-    const double dtir = 2 * T[kTileTir + (g >> 1)];
+    const Phasor hop{T[kTileHopRot + g], T[kTileHopRot + g + 1]};   // 2 * TIR[g / 2]
     for (int hops = 0;; ++hops) {
         if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
         DIAG_REGION(3);   // loop iteration in advance
@@ -478,7 +560,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
         }
         r.x += gx;
         r.y += gy;
-        r.dph += dtir;
+        r.ph = mul(r.ph, hop);
     }
 }
 
@@ -519,14 +601,23 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
                 if (next < 0) break;
                 L.r.region = next;
                 entry = false;
+                DIAG_CLK(ta);
                 do {
                     blk = advance(A, A.loc, L, kind);
                 } while (blk == kTransit);
+                DIAG_CLK(tb);
+                DIAG_ACC(3, ta, tb);
+#ifdef WGRT_TIMERS
+                L.tm[5] += 1;
+#endif
                 if (blk < 0) break;
             }
             lane_retire(A, L);
             b = L.bounces;
             h = L.hit;
+#ifdef WGRT_TIMERS
+            for (int k = 0; k < 6; ++k) atomicAdd(&g_diag_tm[k], (unsigned long long)L.tm[k]);
+#endif
         } else {
             bad = 1;
         }
@@ -581,14 +672,15 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
         uint64_t need = __ballot(!active);
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
-                unsigned long long base = 0;
-                if (lane == 0) base = atomicAdd(counter, (unsigned long long)chunk);
-                base = __shfl(base, 0);
-                if ((int64_t)base >= A.n_rays) {
+                unsigned long long q = 0;
+                if (lane == 0) q = atomicAdd(counter, 1ull);
+                q = __shfl(q, 0);
+                const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
+                if ((int64_t)q >= n_chunks) {
                     exhausted = true;
                     break;
                 }
-                cur = (int64_t)base;
+                cur = (int64_t)(A.order ? A.order[q] : (int64_t)q) * chunk;
                 end = cur + chunk < A.n_rays ? cur + chunk : A.n_rays;
             }
             const int want = __popcll(need);
@@ -655,7 +747,7 @@ __global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, u
     persistent_body(A, A.loc, counter, chunk);
 }
 
-// Variants 4-6: variant 2 at W waves per SIMD (W = 2: register budget 256, no VGPR spills)
+// Variants 4-6: variant 2 at W waves per SIMD (W = 4: register budget 128)
 // and/or with 32-bit cell words in global memory (scenes of <= 16 polygons: half the
 // grid's cache footprint).
 template <class CellT, int W>
@@ -866,7 +958,7 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_kernel, 256, 0));
         s->persistent_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_g_kernel<uint64_t, 2>, 256, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_g_kernel<uint64_t, 4>, 256, 0));
         s->persistent_w2_grid = std::max(1, cus * std::max(1, per_cu));
         if (host.lds.ok) {
             const int bytes = (int)host.lds.bytes.size();
@@ -940,7 +1032,8 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
 // (GRTF:833-1246), threshold 0.  The two kernels differ in nothing else.
 static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
                                 uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
-                                uint32_t *per_ray_bounces, void *stream, int variant, int workgroups, bool single) {
+                                uint32_t *per_ray_bounces, void *stream, int variant, int workgroups, bool single,
+                                const int32_t *chunk_order = nullptr, int64_t n_chunk_order = 0) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
     if (single && s->nl != 1)
@@ -952,6 +1045,7 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     if (variant < 0 || variant > 6) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
     if ((variant == 5 || variant == 6) && !s->d_cells32)
         return fail(WGRT_ERR_UNSUPPORTED, "variants 5 / 6 need <= 16 polygons");
+    if (variant == 0) variant = s->d_cells32 ? 5 : 2;   // auto: the fastest measured
     TraceArgs A;
     A.x = rays->x;
     A.y = rays->y;
@@ -959,6 +1053,15 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.n = rays->n;
     A.l = single ? nullptr : rays->lmd_num;
     A.threshold = single ? 1e-15 : 0.0;
+    A.order = nullptr;
+    if (chunk_order) {
+        // a permutation of the 64-ray chunks (validated by the caller: trusted device data)
+        if (n_chunk_order != (n_rays + kChunk - 1) / kChunk)
+            return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order must list ceil(n_rays / 64) chunks");
+        if (variant == 1)
+            return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order needs a persistent variant");
+        A.order = chunk_order;
+    }
     A.te = rays->te;
     A.tm = rays->tm;
     A.dph = rays->delta_phase;
@@ -1013,7 +1116,7 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
             A.lds.ncx = s->lds.ncx;
             A.lds.ncy = s->lds.ncy;
             hipLaunchKernelGGL(trace_persistent_lds_kernel, dim3((unsigned)grid), dim3(768), (unsigned)s->lds_bytes,
-                               st, A, ctr, 64);
+                               st, A, ctr, kChunk);
         } else if (variant >= 4) {
             LocatorT<uint32_t> l32;
             l32.cells = s->d_cells32;
@@ -1023,16 +1126,16 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
             l32.row_edges = A.loc.row_edges;
             l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
             if (variant == 4)
-                hipLaunchKernelGGL((trace_persistent_g_kernel<uint64_t, 2>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   A.loc, ctr, 64);
+                hipLaunchKernelGGL((trace_persistent_g_kernel<uint64_t, 4>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   A.loc, ctr, kChunk);
             else if (variant == 5)
                 hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   l32, ctr, 64);
+                                   l32, ctr, kChunk);
             else
-                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 2>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   l32, ctr, 64);
+                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 4>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   l32, ctr, kChunk);
         } else {
-            hipLaunchKernelGGL(trace_persistent_kernel, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, 64);
+            hipLaunchKernelGGL(trace_persistent_kernel, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, kChunk);
         }
     }
     HIP_TRY(hipGetLastError());
@@ -1052,6 +1155,15 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *s, const wgrt_rays *rays, int
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream) {
     return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, 0, 0,
                         false);
+}
+
+wgrt_status wgrt_trace_opts(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                            uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                            uint32_t *per_ray_bounces, void *stream, const wgrt_launch_opts *opts) {
+    if (!opts) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL opts");
+    if (opts->kernel != 0 && opts->kernel != 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
+                        opts->variant, opts->workgroups, opts->kernel == 1, opts->chunk_order, opts->n_chunk_order);
 }
 
 wgrt_status wgrt_trace_single_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
@@ -1194,6 +1306,15 @@ const char *wgrt_status_string(wgrt_status s) {
 const char *wgrt_last_error(void) { return g_last_error.c_str(); }
 
 int wgrt_abi_version(void) { return WGRT_ABI_VERSION; }
+
+#if defined(WGRT_DIAG) || defined(WGRT_TIMERS)
+int wgrt_diag_read_timers(unsigned long long *out8) {
+    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_tm), 8 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    unsigned long long z[8] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_tm), z, sizeof(z));
+    return 0;
+}
+#endif
 
 #ifdef WGRT_DIAG
 // Diagnostic build only: read-and-reset the wave-loop counters (synchronous).

@@ -13,12 +13,13 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import Rays, Scene, TraceStats, WgrtError, check, load
+from ._lib import LaunchOpts, Rays, Scene, TraceStats, WgrtError, check, load
 
 RAY_COLUMNS = ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 READ_COLUMNS = ("x", "y", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 
 VARIANT_AUTO, VARIANT_GRID, VARIANT_PERSISTENT = 0, 1, 2
+CHUNK = 64   # rays per work-queue chunk of the persistent kernels (wgrt_launch_opts.chunk_order)
 
 
 def _stream_handle(device: torch.device, stream=None) -> int:
@@ -49,25 +50,26 @@ def rays_to_device(rays: dict, device="cuda") -> dict:
 def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                     gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                     per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                    workgroups: int = 0) -> None:
+                    workgroups: int = 0, chunk_order: torch.Tensor | None = None) -> None:
     """Asynchronous launch on ``stream`` (default: torch's current stream).
 
     rays: dict of device float32 tensors keyed like the reference columns
     (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
     kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
     accepted too.  stats: optional int64[4] device tensor that is added to
-    (bounces, bad_rays, eyebox_hits, reserved).
+    (bounces, bad_rays, eyebox_hits, reserved).  chunk_order: optional int32 device
+    permutation of the 64-ray chunks (``schedule_by_lifetime``); results do not depend on it.
     """
     if scene.single_lambda:
         raise ValueError("trace_fullcolor needs a full-colour scene; use trace_single for a single-wavelength one")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=False)
+           workgroups, single=False, chunk_order=chunk_order)
 
 
 def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                  gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                  per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                 workgroups: int = 0) -> None:
+                 workgroups: int = 0, chunk_order: torch.Tensor | None = None) -> None:
     """One launch of the single-wavelength kernel (``process_rays_kernel_pro``, GRTF:419-831)
     through ``wgrt_trace_single_ex``: no ``lmd_num`` column (ignored if present),
     matrix_EB [NY, NX, 80, 120], branch guard ener * efficiency > 1e-15.  The scene must be
@@ -75,11 +77,11 @@ def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: 
     if not scene.single_lambda:
         raise ValueError("trace_single needs a single-wavelength scene (Scene.from_geometry(..., wavelength=l))")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=True)
+           workgroups, single=True, chunk_order=chunk_order)
 
 
 def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single):
+           workgroups, single, chunk_order=None):
     device = torch.device("cuda", scene.device)
     x = rays["x"]
     N = x.numel() if n_rays is None else int(n_rays)
@@ -107,14 +109,39 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
     r = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in cols.items()})
     for k in ("gap_x", "gap_y", "pol", "azi"):
         setattr(r, k, ctypes.c_void_p(rays[k].data_ptr()) if k in rays else None)
-    fn = load().wgrt_trace_single_ex if single else load().wgrt_trace_fullcolor_ex
-    check(fn(
+    n_chunks = (N + CHUNK - 1) // CHUNK
+    if chunk_order is not None:
+        _as_dev(chunk_order, torch.int32, "chunk_order", device, n_chunks)
+    opts = LaunchOpts(1 if single else 0, int(variant), int(workgroups),
+                      ctypes.c_void_p(chunk_order.data_ptr()) if chunk_order is not None else None,
+                      n_chunks if chunk_order is not None else 0)
+    check(load().wgrt_trace_opts(
         scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
         ctypes.c_void_p(matrix_EB.data_ptr()),
         ctypes.c_void_p(stats.data_ptr()) if stats is not None else None,
         ctypes.c_void_p(per_ray_bounces.data_ptr()) if per_ray_bounces is not None else None,
-        ctypes.c_void_p(_stream_handle(device, stream)), int(variant), int(workgroups)),
+        ctypes.c_void_p(_stream_handle(device, stream)), ctypes.byref(opts)),
         "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
+
+
+def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None):
+    """Issue order of the 64-ray chunks for ``chunk_order``: chunks whose rays belong to the
+    (wavelength, FoV) tiles with the longest mean lifetime in a previous launch go first, so
+    the rays that outlive the work queue come from short-lived tiles and the launch's
+    straggler tail shortens.  ``per_ray_bounces`` from an earlier launch of the same batch
+    (``trace_*(per_ray_bounces=...)``), ``tile_of_ray`` any integer tile key per ray (e.g.
+    ``(lmd_num * NX + m) * NY + n``).  Device tensors in, int32 device permutation out
+    (a few small torch ops, no host sync).  A pure scheduling hint: results are unchanged."""
+    b = per_ray_bounces.to(torch.float32)
+    key = tile_of_ray.to(torch.int64)
+    nt = int(n_tiles) if n_tiles is not None else int(key.max().item()) + 1
+    tot = torch.zeros(nt, dtype=torch.float32, device=b.device).index_add_(0, key, b)
+    cnt = torch.zeros(nt, dtype=torch.float32, device=b.device).index_add_(0, key, torch.ones_like(b))
+    mean = tot / cnt.clamp_min(1.0)
+    N = b.numel()
+    first = torch.arange(0, N, CHUNK, device=b.device)
+    chunk_key = mean[key[first]]
+    return torch.argsort(chunk_key, descending=True, stable=True).to(torch.int32)
 
 
 def init_rays(points, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int, blocks=None,
@@ -174,5 +201,5 @@ def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor
     return out
 
 
-__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "rays_to_device", "classify_points",
+__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "schedule_by_lifetime", "rays_to_device", "classify_points",
            "selftest_math", "RAY_COLUMNS", "_lib"]

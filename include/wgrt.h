@@ -128,10 +128,12 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream);
 
 /* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
- * count for the persistent variant (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
- * grid, 2 persistent wave-refill (locator in global memory), 3 persistent wave-refill with
- * a coarser copy of the locator staged in LDS (needs <= 16 polygons; WGRT_ERR_UNSUPPORTED
- * otherwise).  Auto picks 2.  All variants produce identical results. */
+ * count for the persistent variants (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
+ * grid, 2 persistent wave-refill (locator in global memory, 64-bit cell words), 3 persistent
+ * wave-refill with a coarser copy of the locator staged in LDS, 4 variant 2 at 4 waves per
+ * SIMD, 5 variant 2 with 32-bit cell words, 6 variants 4 + 5.  Variants 3, 5, 6 need <= 16
+ * polygons (WGRT_ERR_UNSUPPORTED otherwise).  Auto picks 5 when possible, else 2.  All
+ * variants produce identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
@@ -151,6 +153,26 @@ wgrt_status wgrt_trace_single_ex(const wgrt_scene *scene, const wgrt_rays *rays,
                                  int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream, int variant,
                                  int workgroups);
+
+/* Launch options for wgrt_trace_opts. */
+typedef struct {
+    int kernel;          /* 0 process_rays_kernel_pro_fullColor, 1 process_rays_kernel_pro (single lambda) */
+    int variant;         /* as wgrt_trace_fullcolor_ex (0 auto)                                           */
+    int workgroups;      /* persistent variants: resident workgroups (0 auto)                             */
+    /* Persistent variants: order in which the 64-ray chunks [64 c, 64 c + 64) are handed to
+     * the waves -- a DEVICE int32 permutation of 0 .. ceil(n_rays / 64) - 1, or NULL for
+     * ascending order.  Results do not depend on it (rays are independent); issuing the
+     * chunks of long-lived rays first shortens the launch's straggler tail (see
+     * engine.schedule_by_lifetime).  The permutation is not validated on the device. */
+    const int32_t *chunk_order;
+    int64_t n_chunk_order;
+} wgrt_launch_opts;
+
+/* One launch of either bounce kernel with launch options (everything else as
+ * wgrt_trace_fullcolor / wgrt_trace_single). */
+wgrt_status wgrt_trace_opts(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                            uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
+                            uint32_t *per_ray_bounces, void *stream, const wgrt_launch_opts *opts);
 
 /* Device-side ray setup (replaces the host loop MAIN:59-115 and the seeding at MAIN:158):
  * fills FoV x wavelength blocks [block_lo, block_hi) of the batch -- block b =
