@@ -172,13 +172,14 @@ def main():
 
 
 def kernel_name(variant, scene):
-    """Name of the kernel a launch runs (wgrt_trace_fullcolor_ex's variant table; auto = 5
-    when the scene has <= 16 polygons, else 2)."""
+    """Name of the kernel a launch runs (wgrt_trace_fullcolor_ex's variant table; auto = 7
+    when the scene has <= 16 polygons, else 9)."""
     if variant == 0:
-        variant = 5 if scene.info()["n_polygons"] <= 16 else 2
+        variant = 7 if scene.info()["n_polygons"] <= 16 else 9
     return {1: "trace_grid_kernel", 2: "trace_persistent_kernel", 3: "trace_persistent_lds_kernel",
             4: "trace_persistent_g_kernel<unsigned long, 4>", 5: "trace_persistent_g_kernel<unsigned int, 3>",
-            6: "trace_persistent_g_kernel<unsigned int, 4>"}[variant]
+            6: "trace_persistent_g_kernel<unsigned int, 4>", 7: "trace_jones_kernel<unsigned int, 3>",
+            8: "trace_jones_kernel<unsigned int, 4>", 9: "trace_jones_kernel<unsigned long, 3>"}[variant]
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):

@@ -52,6 +52,29 @@ constexpr int kTileHeader = 40;
 constexpr int kBlock = 28;        // cosA[3], pad, rec[3][8]
 constexpr int kBlockCos = 0;
 constexpr int kBlockRec = 4;
+
+// ---------------------------------------------------------------------------
+// Jones-vector tile (variants 7-9): the same interaction blocks, laid out in 128-B lines,
+// with the TIR phase step of each taken branch folded into its TM output row (rec q and s
+// multiplied by e^{i lut_TIR[k]}; the branch efficiency |M E|^2 is unchanged by it) and the
+// certification weights of the branch decisions.
+// ---------------------------------------------------------------------------
+constexpr int kJGap = 0;          // lut_gap[8]
+constexpr int kJHop = 8;          // (cos, sin) of 2 lut_TIR[0] (R2 miss hop), of 2 lut_TIR[1] (R3 / R4)
+constexpr int kJCosIc1 = 12;      // cos(lut_ic1[l, m, n, 0].real)
+constexpr int kJGrowth = 13;      // max(1, max_k |lut_TIR[k]| / pi): bounds the reference's unwrapped phase growth
+constexpr int kJHeader = 16;
+constexpr int kJBlock = 32;       // cosA[3], Wsum, rec[3][8], W[3], pad
+constexpr int kJBlockCos = 0;
+constexpr int kJBlockWsum = 3;    // sum of W[k]
+constexpr int kJBlockRec = 4;
+// W[k] = ((|p|+|r|)^2 + (|q|+|s|)^2) * |cosA_k| * f_k (f_k the n_g factor of the branch): for a
+// field state E, |M_k E|^2 * cosA_k * f_k is computed to within D * W[k] * |E|^2 by any two
+// evaluations whose states agree to within D / 4 (relative) -- the bound the Jones-vector
+// variants certify their Monte-Carlo decisions against.
+constexpr int kJBlockW = 28;
+WGRT_HD int jtile_doubles(int nfc, int noc) { return kJHeader + kJBlock * (3 + 2 * nfc + 2 * noc); }
+
 // block index: 0 in-coupling, 1 R0, 2 R1, 3 + k R2 slice k, 3 + nfc + k R3,
 //              3 + 2 nfc + k R4, 3 + 2 nfc + noc + k R5
 WGRT_HD int tile_doubles(int nfc, int noc) { return kTileHeader + kBlock * (3 + 2 * nfc + 2 * noc); }

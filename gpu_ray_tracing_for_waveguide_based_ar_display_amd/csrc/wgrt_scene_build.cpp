@@ -303,6 +303,58 @@ void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles) {
             }
 }
 
+void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std::vector<double> &jt) {
+    const int64_t L = d.num_lmd, NX = d.nx, NY = d.ny;
+    const int nfc = (int)d.n_fc_slices, noc = (int)d.n_oc_slices;
+    const int TD = tile_doubles(nfc, noc), JD = jtile_doubles(nfc, noc);
+    const int nblk = 3 + 2 * nfc + 2 * noc;
+    jt.assign((size_t)(L * NX * NY) * JD, 0.0);
+    for (int64_t g = 0; g < L * NX * NY; ++g) {
+        const double *T = tiles.data() + (size_t)g * TD;
+        double *J = jt.data() + (size_t)g * JD;
+        const double *tir = d.lut_TIR + 4 * g;
+        for (int k = 0; k < 8; ++k) J[kJGap + k] = T[kTileGap + k];
+        for (int k = 0; k < 4; ++k) J[kJHop + k] = T[kTileHopRot + k];
+        J[kJCosIc1] = T[kTileCosIc1];
+        double tir_max = 0.0;
+        for (int k = 0; k < 4; ++k) tir_max = std::max(tir_max, std::fabs(tir[k]));
+        J[kJGrowth] = std::max(1.0, tir_max / kPi);
+        for (int b = 0; b < nblk; ++b) {
+            const double *B = T + kTileHeader + kBlock * b;
+            double *O = J + kJHeader + kJBlock * b;
+            const bool three = b >= 3 + 2 * nfc;
+            // TIR step of the taken branches (GRTF:877, 926, 942, 1026, 1039, ...): block 0-2 (IC
+            // states) TIR[0] / TIR[2], FC blocks TIR[0] / TIR[1], OC blocks TIR[1] / TIR[3]
+            const int ta = b < 3 ? 0 : (three ? 1 : 0), tb = b < 3 ? 2 : (three ? 3 : 1);
+            double sum = 0.0;
+            for (int k = 0; k < 3; ++k) {
+                O[kJBlockCos + k] = B[kBlockCos + k];
+                double *rec = O + kJBlockRec + 8 * k;
+                for (int j = 0; j < 8; ++j) rec[j] = B[kBlockRec + 8 * k + j];
+                double w = 0.0;
+                if (k < 2 || three) {
+                    const double p = std::hypot(rec[0], rec[1]), q = std::hypot(rec[2], rec[3]);
+                    const double r = std::hypot(rec[4], rec[5]), s = std::hypot(rec[6], rec[7]);
+                    const double f = (b == 0) ? d.n_g : (k == 2 ? 1.0 / d.n_g : 1.0);
+                    // 1.01: covers the rounding of this bound itself
+                    w = ((p + r) * (p + r) + (q + s) * (q + s)) * std::fabs(B[kBlockCos + k]) * f * 1.01;
+                }
+                if (k < 2) {   // turn the TM output row (q, s) by e^{i lut_TIR[t]}
+                    const double th = tir[k == 0 ? ta : tb], c = std::cos(th), sn = std::sin(th);
+                    for (int j : {2, 6}) {
+                        const double re = rec[j], im = rec[j + 1];
+                        rec[j] = re * c - im * sn;
+                        rec[j + 1] = re * sn + im * c;
+                    }
+                }
+                O[kJBlockW + k] = w;
+                sum += w;
+            }
+            O[kJBlockWsum] = sum * 1.01;
+        }
+    }
+}
+
 void validate_desc(const wgrt_scene_desc &d) {
     check(d.num_lmd > 0 && d.nx > 0 && d.ny > 0, "num_lmd, nx, ny must be positive");
     check(d.n_fc_slices >= 0 && d.n_oc_slices >= 0, "slice counts must be >= 0");
@@ -386,10 +438,12 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) 
     build_locator(polys, nv, cell_mm, out.loc);
     build_lds_image(polys, nv, 2 * cell_mm, kLdsBudget, out.lds);
     pack_tiles(d, out.tiles);
+    pack_jtiles(d, out.tiles, out.jtiles);
     // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would
     // make the reference's efficiencies NaN); such LUTs are rejected instead.
     for (const double v : out.tiles) check(std::isfinite(v), "non-finite value in the LUTs / lut_TIR / lut_gap / eyebox tables");
     out.tile_doubles = tile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
+    out.jtile_doubles = jtile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
 }
 
 }  // namespace wgrt

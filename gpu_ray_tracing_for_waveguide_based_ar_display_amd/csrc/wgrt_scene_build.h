@@ -37,11 +37,14 @@ struct SceneHost {
     LdsImage lds;
     std::vector<double> tiles;     // [num_lmd * nx * ny][tile_doubles]
     int tile_doubles = 0;
+    std::vector<double> jtiles;    // [num_lmd * nx * ny][jtile_doubles] (Jones-vector variants)
+    int jtile_doubles = 0;
 };
 
 void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
                    double cell_mm, LocatorHost &out);
 void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles);
+void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std::vector<double> &jtiles);
 void validate_desc(const wgrt_scene_desc &d);
 void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out);
 // Largest-resolution locator image (cell size cell_mm * 2^k) that fits in max_bytes.

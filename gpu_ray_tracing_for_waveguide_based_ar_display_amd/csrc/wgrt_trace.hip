@@ -28,6 +28,7 @@
 #include <cstdlib>
 #include <cstring>
 #include <algorithm>
+#include <map>
 #include <atomic>
 #include <cmath>
 #include <mutex>
@@ -37,6 +38,10 @@
 #include "../../include/wgrt.h"
 #include "wgrt_common.h"
 #include "wgrt_scene_build.h"
+
+#ifndef WGRT_W8
+#define WGRT_W8 4   // waves per SIMD of variant 8
+#endif
 
 using namespace wgrt;
 
@@ -53,6 +58,7 @@ double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
     return v ? atof(v) : 0.015625;   // 1/64 mm: 37 MB grid at the reference design; fastest on C3
 }();
+double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
 int g_max_hops = [] {
     const char *v = getenv("WGRT_MAX_HOPS");
     return v ? atoi(v) : 2;
@@ -77,6 +83,7 @@ wgrt_status fail(wgrt_status s, const std::string &msg) {
 // copy (up to 32 polygons), uint32_t for the LDS-resident copy (up to 16 polygons).
 template <class CellT>
 struct LocatorT {
+    using Word = CellT;
     const CellT *cells;
     const double *verts;
     const int32_t *poly_off;
@@ -112,6 +119,15 @@ struct TraceArgs {
     double threshold;   // ener * efficiency > threshold guard of R2..R5: 0 full colour, 1e-15 single lambda
     const int32_t *order;   // persistent variants: issue order of the 64-ray chunks (NULL: ascending)
     int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
+    const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
+    int jtile_d;
+    // Jones-vector variants: out-couplings, by ray (eb_tag[i] == epoch marks ray i's this launch)
+    double2 *eb_xy;
+    uint32_t *eb_tag;
+    uint32_t epoch;
+    double cert_tol;   // Jones-vector variants: base of the decision certification bound
+    unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
+    uint32_t *replay_list;
 };
 
 constexpr int kPolyEff1 = 0;
@@ -125,11 +141,22 @@ constexpr int kPolyFC0 = 3;
 // 2 take / eyebox, 3 advance, 4 #interactions, 5 #advance calls.
 __device__ unsigned long long g_diag_tm[8];
 #endif
+#ifdef WGRT_PHASES
+// Diagnostic build only (tools/phases.py): shader cycles per persistent-loop phase, summed
+// over waves: [0] advance, [1] refill, [2] interact, [3] passes, [4..7] the same after the work
+// queue ran dry; [8] per-wave start, [9] exhausted, [10] end (s_memrealtime, summed).
+__device__ unsigned long long g_phase[16];
+constexpr int kPhaseWaves = 16384;
+__device__ unsigned long long g_phase_wave_t[kPhaseWaves * 3];
+#endif
 #ifdef WGRT_DIAG
 // Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
 __device__ unsigned long long g_diag[16];
 __device__ unsigned long long g_diag_fallback;
 
+// per-wave timeline (s_memrealtime, 100 MHz): start, queue exhausted, end
+constexpr int kDiagWaves = 16384;
+__device__ unsigned long long g_diag_wave_t[kDiagWaves * 3];
 // region r: g_diag[6 + r] += number of wave executions, g_diag_act[r] += active lanes
 __device__ unsigned long long g_diag_act[16];
 __device__ __forceinline__ void diag_region(int r) {
@@ -189,6 +216,49 @@ __device__ __forceinline__ int first_slice(const Loc &L, const Cell &c, int firs
         const int s = p >> 1;
         if ((in >> p) & 1ull) return s;
         if (in_poly(L, c, first + s, x, y)) return s;
+        cand &= cand - 1ull;
+    }
+    return -1;
+}
+
+// Word-only forms for the Jones-vector lane: a cell is just its class word (the row of an
+// EDGE cell is recomputed from y on the rare exact test), which keeps prefetched cells in one
+// register each.
+template <class Loc>
+__device__ __forceinline__ typename Loc::Word locate_w(const Loc &L, double x, double y) {
+    const double fx = floor((x - L.x0) * L.inv_h);
+    const double fy = floor((y - L.y0) * L.inv_h);
+    if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return 0;
+    return L.cells[(int)fy * L.ncx + (int)fx];
+}
+
+template <class Loc>
+__device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y) {
+    const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
+    if (cls != 2u) return cls == 1u;
+#ifdef WGRT_ABL_EDGE
+    return false;   // ablation build only: EDGE cells count as outside
+#endif
+    DIAG_REGION(4);
+    const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
+    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
+    const int r = k * L.ncy + cy;
+    const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
+    return inside_or_on_edge_subset(x, y, L.verts + 2 * a, nv, L.row_edges + e0, e1 - e0);
+}
+
+template <class Loc>
+__device__ __forceinline__ int first_slice_w(const Loc &L, typename Loc::Word w, int first, int count, double x,
+                                             double y) {
+    uint64_t f = (uint64_t)w >> (2 * first);
+    if (count < 32) f &= (1ull << (2 * count)) - 1ull;
+    const uint64_t in = f & 0x5555555555555555ull;
+    uint64_t cand = in | ((f >> 1) & 0x5555555555555555ull);
+    while (cand != 0ull) {
+        const int p = __builtin_ctzll(cand);
+        const int sl = p >> 1;
+        if ((in >> p) & 1ull) return sl;
+        if (in_poly_w(L, w, first + sl, x, y)) return sl;
         cand &= cand - 1ull;
     }
     return -1;
@@ -287,7 +357,7 @@ struct Lane {
 // FoV / wavelength indices fall outside the scene.
 __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L) {
 #ifdef WGRT_ABL_RAYLOAD
-    const int64_t ld = i & 1023;   // ablation build only: ray inputs from a cache-hot window
+    const int64_t ld = (i & 63) | (i & ~(int64_t)1023);   // ablation build only: 64 cache-hot rays per block
 #else
     const int64_t ld = i;
 #endif
@@ -564,7 +634,316 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     }
 }
 
-__device__ __forceinline__ void lane_retire(const TraceArgs &A, const Lane &L) {
+// ----------------------------------------------------------------------------
+// Jones-vector path (variants 7-9): certified decisions, side-effect-free abandon + replay
+// ----------------------------------------------------------------------------
+// The reference carries a ray's polarisation as (|Ete|, |Etm|, delta_phase) and re-derives it
+// at every taken branch through hypot, atan2 and a wrap (E_field_cal, GRTF:132-152; the
+// branch bodies GRTF:872-882, ...).  Up to a global phase that triple is the Jones vector
+// E = (|Ete|, |Etm| e^{i delta}): E_field_cal applies a 2x2 complex matrix to it, the branch
+// efficiencies are |M E|^2 times a cosine ratio, and taking a branch normalises M E and turns
+// its TM component by e^{i lut_TIR} (a miss hop by e^{2 i lut_TIR}).  These variants carry E
+// itself -- no hypot, atan2, wrap, sin or cos per interaction, one reciprocal square root for
+// the normalisation -- and keep every Monte-Carlo decision the reference's by certifying it:
+// a decision is taken only when the draw lies farther from every branch threshold than a bound
+// on the difference between this arithmetic and the reference's,
+//     tol = D * |1 / cos(theta)| * max(|E|^2, 1) * sum_k W[k]     (W[k]: wgrt_common.h kBlockW),
+//     D   = cert_tol * (1 + G (bounces / 100)^2),
+// where cert_tol (1e-10) covers the per-step rounding of both evaluations with a wide margin and
+// the quadratic term the reference's phase, which grows without a wrap over miss hops (G: the
+// tile's max |lut_TIR| / pi).  A ray whose decision cannot be certified (about one in 1e9
+// decisions) is abandoned with no side effect -- its RNG state, counters and eyebox cells are
+// written only when it terminates -- and re-traced from its launch-start state by the
+// reference-arithmetic path (replay_kernel).  Positions, hop counts and eyebox indices are the
+// reference's exact float64 operations, as in every other variant.
+//
+// Latency and issue: a ray's bounces form one dependent chain (cell word -> block -> math ->
+// next position) and a launch's tail is the chain of its longest-lived rays, so every pass is
+// built to wait for one batch of loads: an interaction loads its whole block (the TIR step of
+// each taken branch is pre-folded into the block's TM rows, wgrt_common.h kJ*), the two
+// candidate moves, and issues the cell-word loads of both candidate next positions and of the
+// position one hop beyond each; a miss hop only moves (its phase steps are applied as a power
+// at the next interaction) and issues the cell load two hops ahead.  JLane::pf / pf2 always
+// hold the cell words of the ray's position and of the position one hop further.  Out-coupled
+// rays are queued (position + ray index) and binned into matrix_EB by the epilogue kernel, so
+// the eyebox predicate and its divisions stay out of the wave loop.
+struct JRay {
+    double x, y;
+    double er, ei, mr, mi;   // Jones vector (Ete, Etm), up to a global phase
+    double cos_t, ener;
+    double eerr;             // relative error bound of ener (threshold > 0 kernels only)
+    double gx, gy;           // miss-hop move of the current region
+    uint32_t hops;           // miss hops since the last interaction (phase steps not yet applied)
+    uint32_t s;
+    int region;
+};
+
+struct JLane {
+    JRay r;
+    const double *T;         // this ray's Jones tile
+    int64_t i;
+    uint32_t bounces;
+    uint64_t pf, pf2;        // locator cell words of (x, y) and (x + gx, y + gy)
+};
+
+enum : int { kUncertain = -3 };
+
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L) {
+#ifdef WGRT_ABL_RAYLOAD
+    const int64_t ld = (i & 63) | (i & ~(int64_t)1023);   // ablation build only: 64 cache-hot rays per block
+#else
+    const int64_t ld = i;
+#endif
+    const int m = (int)A.m[ld], n = (int)A.n[ld], l = A.l ? (int)A.l[ld] : 0;
+    if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
+    L.i = i;
+#ifdef WGRT_ABL_TILE
+    L.T = A.jtiles;   // ablation build only: every ray reads tile 0
+#else
+    L.T = A.jtiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d;
+#endif
+    L.r.x = (double)A.x[ld];
+    L.r.y = (double)A.y[ld];
+    const double te = (double)A.te[ld], tm = (double)A.tm[ld];
+    const float d = A.dph[ld];
+    double sd = 0.0, cd = 1.0;
+    if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
+    // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
+    L.r.er = te;
+    L.r.ei = 0.0;
+    L.r.mr = cd * tm;
+    L.r.mi = sd * tm;
+    L.r.cos_t = 1.0;
+    L.r.ener = 1.0;
+    L.r.eerr = 0.0;
+    L.r.gx = L.r.gy = 0.0;
+    L.r.hops = 0;
+    L.r.s = A.rng[ld];
+    L.r.region = 0;
+    L.bounces = 1;
+    L.pf = L.pf2 = 0ull;
+    return true;
+}
+
+struct JField {
+    double er, ei, mr, mi;
+};
+
+struct Rec {
+    double pr, pi, qr, qi, rr, ri, sr, si;
+};
+
+__device__ __forceinline__ Rec load_rec(const double *p) {
+    const double2 a = *(const double2 *)p, b = *(const double2 *)(p + 2);
+    const double2 c = *(const double2 *)(p + 4), d = *(const double2 *)(p + 6);
+    return Rec{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+}
+
+// M E for the coefficients (p, q, r, s) of one E_field_cal call (GRTF:139-144):
+// Ete' = p Ete + r Etm, Etm' = q Ete + s Etm.
+__device__ __forceinline__ JField jones(const Rec &c, const JRay &r) {
+    JField f;
+    f.er = fma(c.pr, r.er, fma(-c.pi, r.ei, fma(c.rr, r.mr, -c.ri * r.mi)));
+    f.ei = fma(c.pr, r.ei, fma(c.pi, r.er, fma(c.rr, r.mi, c.ri * r.mr)));
+    f.mr = fma(c.qr, r.er, fma(-c.qi, r.ei, fma(c.sr, r.mr, -c.si * r.mi)));
+    f.mi = fma(c.qr, r.ei, fma(c.qi, r.er, fma(c.sr, r.mi, c.si * r.mr)));
+    return f;
+}
+
+__device__ __forceinline__ double norm2(const JField &f) {
+    return fma(f.er, f.er, fma(f.ei, f.ei, fma(f.mr, f.mr, f.mi * f.mi)));
+}
+
+// 1 / d and 1 / sqrt(v) to ~1 ulp: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(y, fma(-d, y, 1.0), y);
+    return fma(y, fma(-d, y, 1.0), y);
+}
+
+__device__ __forceinline__ double rsq_nr(double v) {
+    double y = __builtin_amdgcn_rsq(v);
+    const double h = 0.5 * v;
+    y = y * fma(-h * y, y, 1.5);
+    return y * fma(-h * y, y, 1.5);
+}
+
+// Cell word of (x, y): the grid has a border of all-OUT cells, so clamping is exact for points
+// outside it (and for NaN, which converts to 0).
+template <class Loc>
+__device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, double y) {
+    int ix = (int)((x - L.x0) * L.inv_h), iy = (int)((y - L.y0) * L.inv_h);
+    ix = min(max(ix, 0), L.ncx - 1);
+    iy = min(max(iy, 0), L.ncy - 1);
+    return L.cells[iy * L.ncx + ix];
+}
+
+// Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
+// kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
+// of it has been written) and replayed.
+template <class Loc>
+__device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
+                                        bool entry) {
+    JRay &r = L.r;
+    const double *T = L.T;
+    const double *B = T + kJHeader + kJBlock * blk;
+    DIAG_REGION(0);
+    const bool three = kind >= 3;
+    const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
+    // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
+    // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
+    const int ga = kind >= 3 ? 2 : 0;
+    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
+    const double2 mva = *(const double2 *)(T + kJGap + ga), mvb = *(const double2 *)(T + kJGap + gb);
+    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
+    const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
+    const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
+    const Rec k0 = load_rec(B + kJBlockRec), k1 = load_rec(B + kJBlockRec + 8);
+    Rec k2{};
+    if (three) k2 = load_rec(B + kJBlockRec + 16);
+    const double xa = r.x + mva.x, ya = r.y + mva.y;
+    const double xb = r.x + mvb.x, yb = r.y + mvb.y;
+    const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
+    const uint64_t pa2 = locate_c(loc, xa + mva.x, ya + mva.y), pb2 = locate_c(loc, xb + mvb.x, yb + mvb.y);
+
+    // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
+    for (uint32_t h = 0; h < r.hops; ++h) {
+        const double mr = r.mr;
+        r.mr = fma(mr, hop.x, -r.mi * hop.y);
+        r.mi = fma(mr, hop.y, r.mi * hop.x);
+    }
+    r.hops = 0;
+    const double denom = entry ? cg.x : r.cos_t;
+    const double u = rng_draw(r.s, A.gid_offset + L.i);
+    const JField f0 = jones(k0, r), f1 = jones(k1, r);
+    const double q0 = norm2(f0), q1 = norm2(f1);
+    const double q2 = three ? norm2(jones(k2, r)) : 0.0;
+    const double inv = rcp_nr(denom);
+    const double f01 = entry ? A.n_g : 1.0;
+    const double a0 = q0 * cw.x * inv * f01, a1 = q1 * cw.y * inv * f01;
+    const double a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
+    const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
+    const double nb = (double)L.bounces * 0.01;
+    const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
+    const double scl = A.cert_tol * fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double tol = scl * cw.w;
+    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic
+    bool ok = tol > 1e-250 && fabs(u - c0) > tol && fabs(u - c1) > tol && (!three || fabs(u - c2) > tol);
+    const double t = A.threshold;
+    bool p0 = true, p1 = true, p2 = true;
+    if (thr) {
+        if (t == 0.0) {
+            // a branch the certified draw selects has e_k > tol (it lies between two thresholds
+            // more than tol from the draw), so ener * e_k > 0 holds for the reference too unless
+            // that product could underflow
+            ok = ok && r.ener * tol > 1e-290;
+        } else {
+            // ener * e_k > threshold (GRTF:606): certified with ener's tracked relative error
+            const double g0 = r.ener * a0, g1 = r.ener * a1, g2 = r.ener * a2;
+            const double re = r.eerr + 1e-15;
+            const double m0 = re * fabs(g0) + r.ener * scl * B[kJBlockW] * 1.01;
+            const double m1 = re * fabs(g1) + r.ener * scl * B[kJBlockW + 1] * 1.01;
+            const double m2 = re * fabs(g2) + r.ener * scl * B[kJBlockW + 2] * 1.01;
+            p0 = g0 > t;
+            p1 = g1 > t;
+            p2 = g2 > t;
+            ok = ok && (u > c0 || fabs(g0 - t) > m0) && (u > c1 || fabs(g1 - t) > m1) &&
+                 (!three || u > c2 || fabs(g2 - t) > m2);
+        }
+    }
+    if (!ok) return kUncertain;
+    int b;
+    if (u <= c0 && p0) b = 0;
+    else if (u <= c1 && p1) b = 1;
+    else if (three && u <= c2 && p2) b = 2;
+    else return kDie;
+
+    if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240): recorded for the epilogue
+        DIAG_REGION(2);
+        A.eb_xy[L.i] = double2{r.x, r.y};
+        A.eb_tag[L.i] = A.epoch;
+        return kDie;
+    }
+    DIAG_REGION(1);
+    const bool ba = b == 0;
+    const JField f = ba ? f0 : f1;
+    const double n2 = ba ? q0 : q1;
+    if (!(n2 > 1e-300)) return kUncertain;
+    // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
+    const double rn = rsq_nr(n2);
+    r.er = f.er * rn;
+    r.ei = f.ei * rn;
+    r.mr = f.mr * rn;
+    r.mi = f.mi * rn;
+    const double ab = ba ? a0 : a1;
+    if (thr && t != 0.0) r.eerr += scl * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+    r.ener = r.ener * ab;
+    r.cos_t = ba ? cw.x : cw.y;
+    r.x = ba ? xa : xb;
+    r.y = ba ? ya : yb;
+    r.gx = ba ? mva.x : mvb.x;
+    r.gy = ba ? mva.y : mvb.y;
+    L.pf = ba ? pa : pb;
+    L.pf2 = ba ? pa2 : pb2;
+    if (kind == 0) {
+        DIAG_REGION(5);
+        const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
+        if (ba) return in_ic ? 0 : 2;
+        return in_ic ? 1 : kDie;
+    }
+    if (kind <= 2) return ba ? 2 : 3;
+    return ba ? 4 : 5;
+}
+
+// Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
+// that need no Monte-Carlo interaction, at most A.max_hops per call.  Every iteration tests
+// the cell word loaded at least one step earlier (L.pf) and issues the load two hops ahead.
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+    JRay &r = L.r;
+    for (int hops = 0;; ++hops) {
+        if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
+        DIAG_REGION(3);
+        if (L.bounces > (uint32_t)kMaxLoop) return kDie;
+        ++L.bounces;
+        const auto c = (typename Loc::Word)L.pf;
+        if (!in_poly_w(loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        const int region = r.region;
+        if (region <= 1) {
+            kind = 0;
+            return 1 + region;
+        }
+        // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
+        const bool fc = region <= 3;
+        const int first = fc ? kPolyFC0 : kPolyFC0 + A.nfc, count = fc ? A.nfc : A.noc;
+        const int s = first_slice_w(loc, c, first, count, r.x, r.y);
+        if (s >= 0) {
+            kind = region - 1;
+            return (fc ? 3 + (region - 2) * A.nfc : 3 + 2 * A.nfc + (region - 4) * A.noc) + s;
+        }
+        if (region == 5) return kDie;   // GRTF:1244-1246
+        if (region == 3 && !in_poly_w(loc, c, kPolyEff2, r.x, r.y)) {
+            r.region = 4;   // GRTF:1103-1104: no move, same miss hop (gap[2:4], 2 TIR[1])
+            continue;
+        }
+        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178); its phase step waits for the next interaction
+        r.x = r.x + r.gx;
+        r.y = r.y + r.gy;
+        ++r.hops;
+        L.pf = L.pf2;
+        L.pf2 = locate_c(loc, r.x + r.gx, r.y + r.gy);
+    }
+}
+
+__device__ __forceinline__ uint32_t lane_hit(const Lane &L) { return L.hit; }
+__device__ __forceinline__ uint32_t lane_hit(const JLane &) { return 0; }   // counted by the epilogue
+
+template <class LaneT>
+__device__ __forceinline__ void lane_retire(const TraceArgs &A, const LaneT &L) {
+#ifdef WGRT_ABL_NOSTORE
+    if (L.r.s == 0x12345u && L.bounces == 77777u) A.rng[L.i] = 0;   // ablation build only: (almost) no stores
+    return;
+#endif
     A.rng[L.i] = L.r.s;
     if (A.per_ray) A.per_ray[L.i] = L.bounces;
 }
@@ -587,42 +966,85 @@ __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t boun
     }
 }
 
+// Trace ray i to termination with the reference arithmetic (variant 1's lane; replays).
+__device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad) {
+    Lane L;
+    if (!lane_load(A, i, L)) {
+        ++bad;
+        return;
+    }
+    int blk = 0, kind = 0;
+    bool entry = true;
+    for (;;) {
+        const int next = interact(A, A.loc, L, blk, kind, entry);
+        if (next < 0) break;
+        L.r.region = next;
+        entry = false;
+        DIAG_CLK(ta);
+        do {
+            blk = advance(A, A.loc, L, kind);
+        } while (blk == kTransit);
+        DIAG_CLK(tb);
+        DIAG_ACC(3, ta, tb);
+#ifdef WGRT_TIMERS
+        L.tm[5] += 1;
+#endif
+        if (blk < 0) break;
+    }
+    lane_retire(A, L);
+    b += L.bounces;
+    h += L.hit;
+#ifdef WGRT_TIMERS
+    for (int k = 0; k < 6; ++k) atomicAdd(&g_diag_tm[k], (unsigned long long)L.tm[k]);
+#endif
+}
+
 // Variant 1: one ray per lane over a 1-D grid (the reference's launch shape, MAIN:167).
 __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     uint64_t b = 0, h = 0, bad = 0;
-    if (i < A.n_rays) {
-        Lane L;
-        if (lane_load(A, i, L)) {
-            int blk = 0, kind = 0;
-            bool entry = true;
-            for (;;) {
-                const int next = interact(A, A.loc, L, blk, kind, entry);
-                if (next < 0) break;
-                L.r.region = next;
-                entry = false;
-                DIAG_CLK(ta);
-                do {
-                    blk = advance(A, A.loc, L, kind);
-                } while (blk == kTransit);
-                DIAG_CLK(tb);
-                DIAG_ACC(3, ta, tb);
-#ifdef WGRT_TIMERS
-                L.tm[5] += 1;
-#endif
-                if (blk < 0) break;
-            }
-            lane_retire(A, L);
-            b = L.bounces;
-            h = L.hit;
-#ifdef WGRT_TIMERS
-            for (int k = 0; k < 6; ++k) atomicAdd(&g_diag_tm[k], (unsigned long long)L.tm[k]);
-#endif
-        } else {
-            bad = 1;
-        }
-    }
+    if (i < A.n_rays) trace_one(A, i, b, h, bad);
     add_stats(A.stats, b, h, bad);
+}
+
+// Eyebox accumulation of a queued out-coupling (GRTF:1162-1171, 1231-1240): the per-FoV
+// eyebox rectangle test, the bin, and the atomic; compiled-numba addressing as in interact().
+__device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int n, double x, double y) {
+    const double *T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
+    if (!inside_or_on_edge(x, y, T + kTileEbRect, 4)) return false;
+    const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
+    const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
+    const double dx = (xmax - xmin) / kEbNx, dy = (ymax - ymin) / kEbNy;
+    int64_t ix = (int64_t)floor((x - xmin) / dx);
+    int64_t iy = (int64_t)floor((y - ymin) / dy);
+    if (ix < 0) ix += kEbNx;
+    if (iy < 0) iy += kEbNy;
+    const int64_t off = ((((int64_t)l * A.ny + n) * A.nx + m) * kEbNy + iy) * kEbNx + ix;
+    const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
+    if (off < 0 || off >= total) return false;
+    unsafeAtomicAdd(A.eb + off, 1.0f);
+    return true;
+}
+
+// Runs right behind every Jones-vector launch on its stream: bins the queued out-couplings
+// into matrix_EB, and re-traces the rays the launch abandoned (uncertain decisions; nothing of
+// them was written) from their launch-start state with the reference arithmetic.  Usually the
+// replay list is empty.
+__global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
+    const unsigned long long nr = *A.replay_count;
+    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
+    uint64_t b = 0, h = 0, bad = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_rays; i += (int64_t)stride) {
+        if (A.eb_tag[i] != A.epoch) continue;
+        const double2 p = A.eb_xy[i];
+        const int m = (int)A.m[i], n = (int)A.n[i], l = A.l ? (int)A.l[i] : 0;
+        h += eyebox_add(A, l, m, n, p.x, p.y);
+    }
+    for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += stride)
+        trace_one(A, (int64_t)A.replay_list[k], b, h, bad);
+    add_stats(A.stats, b, h, bad);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats && nr)
+        atomicAdd((unsigned long long *)&A.stats->replayed, nr);
 }
 
 // Variant 2: persistent waves with lane refill ("wavefront compaction" of terminated
@@ -634,7 +1056,7 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 // `chunk` consecutive rays from the global counter when the chunk runs dry, and (3) runs
 // the fp64 interaction math for all lanes together.  Results are identical to variant 1:
 // each ray's evolution depends only on its own state and its global index.
-template <class Loc>
+template <class LaneT, class Loc>
 __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &loc, unsigned long long *counter,
                                                 int chunk) {
     const int lane = threadIdx.x & 63;
@@ -642,14 +1064,28 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
     int64_t cur = 0, end = 0;  // wave-uniform chunk cursor
     bool exhausted = false;
     bool active = false;
-    Lane L;
+    LaneT L;
     int blk = 0, kind = 0;
     bool entry = false;
-    uint64_t tot_b = 0, tot_h = 0, tot_bad = 0;
+    uint32_t tot_b = 0, tot_h = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
+#ifdef WGRT_ABL_STATIC
+    int d_static_k = 0;
+#endif
 #ifdef WGRT_DIAG
     uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_hopmax = 0;
+    const int d_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGRT_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int p_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid] = __builtin_amdgcn_s_memrealtime();
 #endif
     for (;;) {
+#ifdef WGRT_PHASES
+        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+        const int pofs = exhausted ? 4 : 0;
+#endif
         if (active) {
 #ifdef WGRT_DIAG
             const uint32_t b0 = L.bounces;
@@ -665,19 +1101,40 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
             if (blk == kDie) {
                 lane_retire(A, L);
                 tot_b += L.bounces;
-                tot_h += L.hit;
+                tot_h += lane_hit(L);
                 active = false;
             }
         }
+#ifdef WGRT_PHASES
+        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
         uint64_t need = __ballot(!active);
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
                 unsigned long long q = 0;
+#ifdef WGRT_ABL_STATIC
+                // ablation build only: wave w takes chunks w, w + W, w + 2W, ... (no atomics)
+                {
+                    const unsigned long long W = (unsigned long long)gridDim.x * (blockDim.x >> 6);
+                    const unsigned long long w = (unsigned long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+                    q = w + W * (unsigned long long)(d_static_k++);
+                }
+#else
                 if (lane == 0) q = atomicAdd(counter, 1ull);
                 q = __shfl(q, 0);
+#endif
                 const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
                 if ((int64_t)q >= n_chunks) {
                     exhausted = true;
+#ifdef WGRT_PHASES
+                    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGRT_DIAG
+                    {
+                        const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+                        if (lane == 0 && wid < kDiagWaves) g_diag_wave_t[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
+                    }
+#endif
                     break;
                 }
                 cur = (int64_t)(A.order ? A.order[q] : (int64_t)q) * chunk;
@@ -704,6 +1161,9 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
             need = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
+#ifdef WGRT_PHASES
+        const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+#endif
 #ifdef WGRT_DIAG
         {
             const uint64_t na = __popcll(__ballot(active));
@@ -717,19 +1177,39 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
 #endif
         if (active && blk >= 0) {
             const int next = interact(A, loc, L, blk, kind, entry);
-            if (next < 0) {
+            if (next == kUncertain) {
+                // abandoned without side effects (Jones-vector variants): replay_kernel re-traces it
+                A.replay_list[atomicAdd(A.replay_count, 1ull)] = (uint32_t)L.i;
+                active = false;
+            } else if (next < 0) {
                 lane_retire(A, L);
                 tot_b += L.bounces;
-                tot_h += L.hit;
+                tot_h += lane_hit(L);
                 active = false;
             } else {
                 L.r.region = next;
             }
         }
+#ifdef WGRT_PHASES
+        {
+            const uint64_t pt3 = __builtin_amdgcn_s_memtime();
+            ph[pofs + 0] += pt1 - pt0;
+            ph[pofs + 1] += pt2 - pt1;
+            ph[pofs + 2] += pt3 - pt2;
+            ph[pofs + 3] += 1;
+        }
+#endif
     }
+#ifdef WGRT_PHASES
+    if (lane == 0) {
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
+        if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
     add_stats(A.stats, tot_b, tot_h, tot_bad);
 #ifdef WGRT_DIAG
     if (lane == 0) {
+        if (d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 2] = __builtin_amdgcn_s_memrealtime();
         atomicAdd(&g_diag[0], d_pass);
         atomicAdd(&g_diag[1], d_act);
         atomicAdd(&g_diag[2], d_pass_x);
@@ -744,7 +1224,7 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
 // Variant 2: the persistent loop with the locator read from global memory (L2-resident).
 __global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, unsigned long long *counter,
                                                                   int chunk) {
-    persistent_body(A, A.loc, counter, chunk);
+    persistent_body<Lane>(A, A.loc, counter, chunk);
 }
 
 // Variants 4-6: variant 2 at W waves per SIMD (W = 4: register budget 128)
@@ -753,7 +1233,15 @@ __global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, u
 template <class CellT, int W>
 __global__ __launch_bounds__(256, W) void trace_persistent_g_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                                     unsigned long long *counter, int chunk) {
-    persistent_body(A, loc, counter, chunk);
+    persistent_body<Lane>(A, loc, counter, chunk);
+}
+
+// Variants 7-9: the persistent loop over the Jones-vector path (32-bit cell words at W waves
+// per SIMD; 64-bit cell words for scenes of more than 16 polygons).
+template <class CellT, int W>
+__global__ __launch_bounds__(256, W) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
+                                                             unsigned long long *counter, int chunk) {
+    persistent_body<JLane>(A, loc, counter, chunk);
 }
 
 // Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
@@ -781,7 +1269,7 @@ __global__ __launch_bounds__(768, 1) void trace_persistent_lds_kernel(TraceArgs 
     loc.inv_h = D.inv_h;
     loc.ncx = D.ncx;
     loc.ncy = D.ncy;
-    persistent_body(A, loc, counter, chunk);
+    persistent_body<Lane>(A, loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -859,6 +1347,8 @@ struct wgrt_scene {
     int nx = 0, ny = 0, nl = 0, nfc = 0, noc = 0, tile_d = 0, npoly = 0;
     double n_g = 0;
     double *d_tiles = nullptr;
+    double *d_jtiles = nullptr;
+    int jtile_d = 0;
     uint64_t *d_cells = nullptr;
     uint32_t *d_cells32 = nullptr;   // 32-bit copy of the cell words (npoly <= 16), else NULL
     double *d_verts = nullptr;
@@ -878,6 +1368,21 @@ struct wgrt_scene {
     char *d_lds_image = nullptr;
     size_t lds_bytes = 0;
     LdsImage lds;              // offsets / grid parameters (bytes released after upload)
+    int jones_grid = 0;        // resident 256-thread workgroups of variant 7
+    int jones_w4_grid = 0;     // ... of variant 8
+    int jones64_grid = 0;      // ... of variant 9
+    // Jones-vector launches: per-stream work counter + replay list (launches on one stream are
+    // ordered, so they may share; launches on different streams never do)
+    struct Scratch {
+        unsigned long long *ctr = nullptr;   // [0] chunk counter, [1] replay count
+        uint32_t *list = nullptr;            // replay list
+        double2 *eb_xy = nullptr;            // out-couplings by ray: position, launch tag
+        uint32_t *eb_tag = nullptr;
+        uint32_t epoch = 0;
+        int64_t cap = 0;
+    };
+    std::mutex scratch_mu;
+    std::map<void *, Scratch> scratch;
 };
 
 namespace {
@@ -929,11 +1434,13 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     s->nfc = (int)desc->n_fc_slices;
     s->noc = (int)desc->n_oc_slices;
     s->tile_d = host.tile_doubles;
+    s->jtile_d = host.jtile_doubles;
     s->npoly = 3 + s->nfc + s->noc;
     s->n_g = desc->n_g;
     s->tiles = (int64_t)s->nl * s->nx * s->ny;
     wgrt_status st;
-    if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK ||
+    if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.jtiles, &s->d_jtiles)) != WGRT_OK ||
+        (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK ||
         (st = upload(host.loc.verts, &s->d_verts)) != WGRT_OK ||
         (st = upload(host.loc.poly_off, &s->d_poly_off)) != WGRT_OK ||
         (st = upload(host.loc.row_off, &s->d_row_off)) != WGRT_OK ||
@@ -960,6 +1467,12 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         s->persistent_grid = std::max(1, cus * std::max(1, per_cu));
         HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_g_kernel<uint64_t, 4>, 256, 0));
         s->persistent_w2_grid = std::max(1, cus * std::max(1, per_cu));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, 3>, 256, 0));
+        s->jones_grid = std::max(1, cus * std::max(1, per_cu));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, WGRT_W8>, 256, 0));
+        s->jones_w4_grid = std::max(1, cus * std::max(1, per_cu));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint64_t, 3>, 256, 0));
+        s->jones64_grid = std::max(1, cus * std::max(1, per_cu));
         if (host.lds.ok) {
             const int bytes = (int)host.lds.bytes.size();
             int lds_max = 0;
@@ -999,6 +1512,7 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     if (!s) return WGRT_OK;
     (void)hipSetDevice(s->device);
     (void)hipFree(s->d_tiles);
+    (void)hipFree(s->d_jtiles);
     (void)hipFree(s->d_cells);
     (void)hipFree(s->d_cells32);
     (void)hipFree(s->d_verts);
@@ -1007,6 +1521,12 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_row_off);
     (void)hipFree(s->d_row_edges);
     (void)hipFree(s->d_lds_image);
+    for (auto &kv : s->scratch) {
+        (void)hipFree(kv.second.ctr);
+        (void)hipFree(kv.second.list);
+        (void)hipFree(kv.second.eb_xy);
+        (void)hipFree(kv.second.eb_tag);
+    }
     delete s;
     return WGRT_OK;
 }
@@ -1042,10 +1562,12 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     if (!rays->x || !rays->y || !rays->m || !rays->n || (!single && !rays->lmd_num) || !rays->te || !rays->tm ||
         !rays->delta_phase || !rng_states || !matrix_EB)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL ray column / rng_states / matrix_EB");
-    if (variant < 0 || variant > 6) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
-    if ((variant == 5 || variant == 6) && !s->d_cells32)
-        return fail(WGRT_ERR_UNSUPPORTED, "variants 5 / 6 need <= 16 polygons");
-    if (variant == 0) variant = s->d_cells32 ? 5 : 2;   // auto: the fastest measured
+    if (variant < 0 || variant > 9) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
+    if ((variant == 5 || variant == 6 || variant == 7 || variant == 8) && !s->d_cells32)
+        return fail(WGRT_ERR_UNSUPPORTED, "variants 5-8 need <= 16 polygons");
+    if (variant >= 7 && n_rays > 0xffffffffll)
+        return fail(WGRT_ERR_UNSUPPORTED, "variants 7-9 index at most 2^32 - 1 rays per launch");
+    if (variant == 0) variant = s->d_cells32 ? 7 : (n_rays <= 0xffffffffll ? 9 : 2);   // auto
     TraceArgs A;
     A.x = rays->x;
     A.y = rays->y;
@@ -1083,8 +1605,78 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
     A.max_hops = g_max_hops;
+    A.cert_tol = g_cert_tol;
+    A.replay_count = nullptr;
+    A.replay_list = nullptr;
+    A.jtiles = s->d_jtiles;
+    A.jtile_d = s->jtile_d;
+    A.eb_xy = nullptr;
+    A.eb_tag = nullptr;
+    A.epoch = 0;
     hipStream_t st = (hipStream_t)stream;
-    if (variant == 1) {
+    if (variant >= 7) {
+        wgrt_scene *ms = const_cast<wgrt_scene *>(s);
+        wgrt_scene::Scratch *sc;
+        {
+            std::lock_guard<std::mutex> lk(ms->scratch_mu);
+            sc = &ms->scratch[stream];
+            if (!sc->ctr) {
+                hipError_t e = hipMalloc((void **)&sc->ctr, 2 * sizeof(unsigned long long));
+                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+            }
+            if (sc->cap < n_rays) {
+                // the old lists may still be in use by this stream's previous launch
+                HIP_TRY(hipStreamSynchronize(st));
+                (void)hipFree(sc->list);
+                (void)hipFree(sc->eb_xy);
+                (void)hipFree(sc->eb_tag);
+                sc->list = sc->eb_tag = nullptr;
+                sc->eb_xy = nullptr;
+                sc->cap = 0;
+                sc->epoch = 0;
+                hipError_t e = hipMalloc((void **)&sc->list, (size_t)n_rays * sizeof(uint32_t));
+                if (e == hipSuccess) e = hipMalloc((void **)&sc->eb_xy, (size_t)n_rays * sizeof(double2));
+                if (e == hipSuccess) e = hipMalloc((void **)&sc->eb_tag, (size_t)n_rays * sizeof(uint32_t));
+                if (e == hipSuccess) e = hipMemset(sc->eb_tag, 0, (size_t)n_rays * sizeof(uint32_t));
+                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+                sc->cap = n_rays;
+            }
+        }
+        A.replay_count = sc->ctr + 1;
+        A.replay_list = sc->list;
+        if (++sc->epoch == 0) {   // tags wrapped (after 2^32 launches): clear them
+            HIP_TRY(hipMemsetAsync(sc->eb_tag, 0, (size_t)sc->cap * sizeof(uint32_t), st));
+            sc->epoch = 1;
+        }
+        A.eb_xy = sc->eb_xy;
+        A.eb_tag = sc->eb_tag;
+        A.epoch = sc->epoch;
+        HIP_TRY(hipMemsetAsync(sc->ctr, 0, 2 * sizeof(unsigned long long), st));
+        int64_t grid = workgroups > 0 ? workgroups
+                                      : (variant == 7 ? s->jones_grid : variant == 8 ? s->jones_w4_grid : s->jones64_grid);
+        const int64_t useful = (n_rays + 255) / 256;
+        if (grid > useful) grid = useful;
+        LocatorT<uint32_t> l32;
+        l32.cells = s->d_cells32;
+        l32.verts = A.loc.verts;
+        l32.poly_off = A.loc.poly_off;
+        l32.row_off = A.loc.row_off;
+        l32.row_edges = A.loc.row_edges;
+        l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
+        if (variant == 7)
+            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
+                               sc->ctr, kChunk);
+        else if (variant == 8)
+            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, WGRT_W8>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
+                               sc->ctr, kChunk);
+        else
+            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, A.loc,
+                               sc->ctr, kChunk);
+        HIP_TRY(hipGetLastError());
+        const int64_t eblocks = std::min<int64_t>((n_rays + 255) / 256, 2048);
+        hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
+    } else if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
         if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
         hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
@@ -1292,6 +1884,12 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
     return WGRT_OK;
 }
 
+double wgrt_debug_set_cert_tol(double cert_tol) {
+    const double prev = g_cert_tol;
+    if (cert_tol > 0.0) g_cert_tol = cert_tol;
+    return prev;
+}
+
 const char *wgrt_status_string(wgrt_status s) {
     switch (s) {
         case WGRT_OK: return "ok";
@@ -1306,6 +1904,18 @@ const char *wgrt_status_string(wgrt_status s) {
 const char *wgrt_last_error(void) { return g_last_error.c_str(); }
 
 int wgrt_abi_version(void) { return WGRT_ABI_VERSION; }
+
+#ifdef WGRT_PHASES
+int wgrt_diag_read_phases(unsigned long long *out16, unsigned long long *wave_t) {
+    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), 16 * sizeof(unsigned long long)) != hipSuccess) return 2;
+    if (hipMemcpyFromSymbol(wave_t, HIP_SYMBOL(g_phase_wave_t), sizeof(g_phase_wave_t)) != hipSuccess) return 2;
+    unsigned long long z[16] = {0};
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z));
+    std::vector<unsigned long long> zw(kPhaseWaves * 3, 0ull);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_wave_t), zw.data(), sizeof(g_phase_wave_t));
+    return 0;
+}
+#endif
 
 #if defined(WGRT_DIAG) || defined(WGRT_TIMERS)
 int wgrt_diag_read_timers(unsigned long long *out8) {
@@ -1322,6 +1932,13 @@ int wgrt_diag_read_regions(unsigned long long *out16) {
     if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_diag_act), 16 * sizeof(unsigned long long)) != hipSuccess) return 2;
     unsigned long long z[16] = {0};
     (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_act), z, sizeof(z));
+    return 0;
+}
+
+int wgrt_diag_read_wave_times(unsigned long long *out) {   // kDiagWaves * 3, then reset
+    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_wave_t), sizeof(g_diag_wave_t)) != hipSuccess) return 2;
+    std::vector<unsigned long long> z(kDiagWaves * 3, 0ull);
+    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_wave_t), z.data(), sizeof(g_diag_wave_t));
     return 0;
 }
 

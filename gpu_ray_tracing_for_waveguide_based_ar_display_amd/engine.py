@@ -57,7 +57,7 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
     (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
     kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
     accepted too.  stats: optional int64[4] device tensor that is added to
-    (bounces, bad_rays, eyebox_hits, reserved).  chunk_order: optional int32 device
+    (bounces, bad_rays, eyebox_hits, replayed).  chunk_order: optional int32 device
     permutation of the 64-ray chunks (``schedule_by_lifetime``); results do not depend on it.
     """
     if scene.single_lambda:

@@ -93,7 +93,8 @@ typedef struct {
     uint64_t bounces;      /* ray-bounce events: 1 in-coupling + loop iterations, per ray */
     uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num               */
     uint64_t eyebox_hits;  /* rays accumulated into matrix_EB                             */
-    uint64_t reserved;
+    uint64_t replayed;     /* Jones-vector variants: rays abandoned on an uncertain decision and
+                              re-traced with the reference arithmetic (included in the counts above) */
 } wgrt_trace_stats;
 
 typedef struct {
@@ -131,9 +132,14 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
  * count for the persistent variants (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
  * grid, 2 persistent wave-refill (locator in global memory, 64-bit cell words), 3 persistent
  * wave-refill with a coarser copy of the locator staged in LDS, 4 variant 2 at 4 waves per
- * SIMD, 5 variant 2 with 32-bit cell words, 6 variants 4 + 5.  Variants 3, 5, 6 need <= 16
- * polygons (WGRT_ERR_UNSUPPORTED otherwise).  Auto picks 5 when possible, else 2.  All
- * variants produce identical results. */
+ * SIMD, 5 variant 2 with 32-bit cell words, 6 variants 4 + 5; 7 / 8 the persistent loop over
+ * the Jones-vector state with certified decisions (32-bit cell words, 3 / 4 waves per SIMD),
+ * 9 the same with 64-bit cell words.  Variants 7-9 re-trace the rays whose decision they cannot
+ * certify with the reference arithmetic in a second kernel on the same stream
+ * (wgrt_trace_stats.replayed counts them); the first such launch on a stream allocates a
+ * per-stream scratch list of n_rays entries.  Variants 3, 5-8 need <= 16 polygons
+ * (WGRT_ERR_UNSUPPORTED otherwise).  Auto picks 7 when possible, else 9.  All variants produce
+ * identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
@@ -200,6 +206,11 @@ wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64
  * and classifies n HOST points exactly as the kernels do. */
 wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, int which, const double *xy,
                                        int64_t n, uint64_t *out_mask);
+
+/* Test hook: base of the Jones-vector variants' decision certification bound (default 1e-10;
+ * larger values make more decisions uncertain and send more rays through the replay kernel,
+ * results unchanged).  Process-wide; returns the previous value. */
+double wgrt_debug_set_cert_tol(double cert_tol);
 
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */

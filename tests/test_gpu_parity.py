@@ -53,7 +53,10 @@ def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0):
 from tests._fixtures import CASES, GoldenCase  # noqa: E402
 
 
-@pytest.mark.parametrize("variant", [1, 2, 3])
+VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]   # 0 = auto (what trace_fullcolor runs by default)
+
+
+@pytest.mark.parametrize("variant", VARIANTS)
 @pytest.mark.parametrize("name", CASES)
 def test_golden_exact(dev, name, variant):
     case = GoldenCase(name)
@@ -99,7 +102,7 @@ def _config(nx, ny, lambdas, R, seed=0, profile="default", point_seed=1, wavelen
     dict(nx=11, ny=11, lambdas=[1], R=1024, wavelength=1),           # single-wavelength kernel, C2 size
     dict(nx=7, ny=7, lambdas=[2], R=512, profile="balanced", gap_scale=0.25, wavelength=2),  # 1e-15 guard
 ])
-@pytest.mark.parametrize("variant", [1, 2, 3])
+@pytest.mark.parametrize("variant", VARIANTS)
 def test_matches_oracle_at_scale(dev, cfg, variant):
     from oracle import OracleScene
     c = _config(**cfg)
@@ -114,6 +117,43 @@ def test_matches_oracle_at_scale(dev, cfg, variant):
         np.testing.assert_array_equal(res[it]["eb"], eb)
         assert int(res[it]["stats"][0]) == tot
         assert int(res[it]["stats"][2]) == int(round(float(eb.sum()) - float(res[it - 1]["eb"].sum() if it else 0)))
+
+
+@pytest.mark.parametrize("cert_tol", [1e-4, 1e-2])
+@pytest.mark.parametrize("cfg", [dict(nx=11, ny=11, lambdas=[1], R=256),
+                                 dict(nx=9, ny=7, lambdas=[0, 1, 2], R=256, profile="deep", seed=5),
+                                 dict(nx=7, ny=7, lambdas=[2], R=512, profile="balanced", gap_scale=0.25,
+                                      wavelength=2)])
+def test_replay_path_forced(dev, cfg, cert_tol):
+    """The Jones-vector variants' rare branch (SURVEY-style rule: a rare data-dependent branch
+    needs its own test): a large certification bound makes many decisions uncertain, so many
+    rays are abandoned and re-traced by replay_kernel -- results must still equal the oracle
+    bit for bit, and the replay counter must show the branch ran."""
+    from oracle import OracleScene
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
+    c = _config(**cfg)
+    prev = _lib.load().wgrt_debug_set_cert_tol(cert_tol)
+    try:
+        res = _trace_case(c, dev, 2, variant=7)
+    finally:
+        _lib.load().wgrt_debug_set_cert_tol(prev)
+    sc = OracleScene.from_geometry(c.geom, c.luts, wavelength=c.wavelength)
+    rng = c.fresh_rng()
+    eb = np.zeros(c.eb_shape(), np.float32)
+    for it in range(2):
+        tot, per = sc.trace(c.rays, rng, eb, per_ray_bounces=True)
+        np.testing.assert_array_equal(res[it]["bounces"], per)
+        np.testing.assert_array_equal(res[it]["rng"], rng)
+        np.testing.assert_array_equal(res[it]["eb"], eb)
+        assert int(res[it]["stats"][0]) == tot
+        assert int(res[it]["stats"][3]) > 0.01 * c.N * min(1.0, cert_tol * 100)   # replays happened
+
+
+def test_replay_rare_at_default_bound(dev):
+    """At the default bound replays are rare (about one per 1e9 decisions)."""
+    c = _config(21, 21, [0, 1, 2], 256)
+    res = _trace_case(c, dev, 1, per_ray=False, variant=7)
+    assert int(res[0]["stats"][3]) <= 2
 
 
 def test_sharding_invariance_gpu(dev):

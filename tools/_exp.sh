@@ -1,10 +1,8 @@
 #!/bin/bash
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
-timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -3 gpurun_out/pytest_gpu.log
+timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread > gpurun_out/pytest_exp.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_exp.log
 if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 300 python tools/ab.py --variants 2,1,3,4,5,6 --rounds 10 > gpurun_out/ab.log 2>&1 || exit $?
-timeout -k 10 600 python tools/ab_libs.py --rounds 3 abl/old.so abl/est.so abl/phasor.so > gpurun_out/ab_libs.log 2>&1 || exit $?
-timeout -k 10 300 python tools/latency_probe.py > gpurun_out/latency.log 2>&1 || exit $?
-echo done
+timeout -k 10 200 python tools/ab.py --variants 5,7 --rounds 8 > gpurun_out/ab.log 2>&1 || exit $?
+timeout -k 10 200 python tools/phases.py 7 > gpurun_out/phases7.log 2>&1 || exit $?

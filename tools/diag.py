@@ -41,9 +41,17 @@ st = torch.zeros(4, dtype=torch.int64, device=dev)
 L = _lib._lib
 L.wgrt_diag_read.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 buf = (ctypes.c_ulonglong * 17)()
+acts = (ctypes.c_ulonglong * 16)()
+L.wgrt_diag_read_wave_times.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+L.wgrt_diag_read_regions.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+# warm-up launch (caches, clocks), counters discarded
+trace_fullcolor(scene, rays, rng.clone(), eb.clone(), variant=variant)
+torch.cuda.synchronize()
+L.wgrt_diag_read(buf)
+L.wgrt_diag_read_regions(acts)
+L.wgrt_diag_read_wave_times((ctypes.c_ulonglong * (16384 * 3))())
 trace_fullcolor(scene, rays, rng, eb, stats=st, variant=variant)
 torch.cuda.synchronize()
-acts = (ctypes.c_ulonglong * 16)()
 L.wgrt_diag_read_regions.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 L.wgrt_diag_read_regions(acts)
 L.wgrt_diag_read(buf)
@@ -54,6 +62,20 @@ print(f"passes={d[0]} mean_active_at_interact={d[1] / max(d[0], 1):.1f}/64 "
       f"passes_after_exhaust={d[2]} ({d[2] / max(d[0], 1):.1%}) mean_active_after={d[3] / max(d[2], 1):.1f}")
 print(f"lane_hops={d[4]} hops/pass(lane-mean)={d[4] / max(d[1], 1):.2f} simt_hop_cost/pass={d[5] / max(d[0], 1):.2f} "
       f"exact_fallbacks={d[16]} interactions~={d[1]}")
+wt = (ctypes.c_ulonglong * (16384 * 3))()
+L.wgrt_diag_read_wave_times.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
+L.wgrt_diag_read_wave_times(wt)
+w = np.array(wt, dtype=np.float64).reshape(-1, 3)
+w = w[w[:, 0] > 0]
+if len(w):
+    t0 = w[:, 0].min()
+    st, ex, en = (w[:, 0] - t0) / 100.0, (w[:, 1] - t0) / 100.0, (w[:, 2] - t0) / 100.0   # us
+    ex = np.where(w[:, 1] > 0, ex, en)
+    q = lambda a: " ".join(f"{v:.1f}" for v in np.percentile(a, [0, 10, 50, 90, 100]))
+    print(f"waves={len(w)} start us [p0 p10 p50 p90 max]: {q(st)}")
+    print(f"  queue-exhausted us: {q(ex)}")
+    print(f"  end us:             {q(en)}")
+    print(f"  tail (end - exhausted) us: {q(en - ex)}")
 for r, name in enumerate(["interact", "take", "eyebox", "advance-iter", "edge-test", "ic-check", "refill-load"]):
     n, act = d[6 + r], acts[r]
     print(f"  region {name:13s} wave-execs={n:9d} mean_active={act / max(n, 1):5.1f}/64")

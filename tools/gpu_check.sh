@@ -14,7 +14,7 @@ ok_or_stop() {  # $1 = exit code, $2 = step name
 }
 STEPS=${STEPS:-pytest,smoke,traffic,bench,prof}
 if [[ $STEPS == *pytest* ]]; then
-  timeout -k 10 1200 python -m pytest tests -m gpu -q -rf ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
+  timeout -k 10 1200 python -u -m pytest tests -m gpu -q -rf --timeout 300 --timeout-method thread ${PYTEST_ARGS:-} > "$OUT/pytest_gpu.log" 2>&1
   ok_or_stop $? pytest
 fi
 if [[ $STEPS == *smoke* ]]; then
@@ -30,9 +30,20 @@ if [[ $STEPS == *bench* ]]; then
   ok_or_stop $? bench
 fi
 if [[ $STEPS == *prof* ]]; then
-  cd /tmp
-  timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline --traffic-json "$OUT/hbm_traffic.json" ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1
+  (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- \
+    python3 "$ROOT/bench.py" --no-cpu-baseline --traffic-json "$OUT/hbm_traffic.json" ${BENCH_ARGS:-} > "$OUT/bench_prof.log" 2>&1)
   ok_or_stop $? prof
+fi
+if [[ $STEPS == *diag* ]]; then
+  timeout -k 10 300 python tools/diag.py 1024 ${DIAG_VARIANT:-0} > "$OUT/diag.log" 2>&1
+  ok_or_stop $? diag
+fi
+if [[ $STEPS == *ab* ]]; then
+  timeout -k 10 300 python tools/ab.py --variants ${AB_VARIANTS:-0,2,5,6} --rounds 10 > "$OUT/ab.log" 2>&1
+  ok_or_stop $? ab
+fi
+if [[ $STEPS == *latency* ]]; then
+  timeout -k 10 300 python tools/latency_probe.py > "$OUT/latency.log" 2>&1
+  ok_or_stop $? latency
 fi
 exit 0
