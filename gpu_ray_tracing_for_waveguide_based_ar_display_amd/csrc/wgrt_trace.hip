@@ -58,6 +58,18 @@ double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
     return v ? atof(v) : 0.015625;   // 1/64 mm: 37 MB grid at the reference design; fastest on C3
 }();
+// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK, multiple of 64)
+int g_jchunk = [] {
+    const char *v = getenv("WGRT_JCHUNK");
+    const int c = v ? atoi(v) : 64;
+    return c >= 64 ? c / 64 * 64 : 64;
+}();
+// miss hops per pass of the Jones-vector variants (env WGRT_JMAX_HOPS; 1 measured best on C3:
+// every hop then tests a cell word loaded at least a pass earlier)
+int g_jmax_hops = [] {
+    const char *v = getenv("WGRT_JMAX_HOPS");
+    return v ? atoi(v) : 1;
+}();
 double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
 int g_max_hops = [] {
     const char *v = getenv("WGRT_MAX_HOPS");
@@ -146,6 +158,7 @@ __device__ unsigned long long g_diag_tm[8];
 // over waves: [0] advance, [1] refill, [2] interact, [3] passes, [4..7] the same after the work
 // queue ran dry; [8] per-wave start, [9] exhausted, [10] end (s_memrealtime, summed).
 __device__ unsigned long long g_phase[16];
+
 constexpr int kPhaseWaves = 16384;
 __device__ unsigned long long g_phase_wave_t[kPhaseWaves * 3];
 #endif
@@ -661,10 +674,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
 // next position) and a launch's tail is the chain of its longest-lived rays, so every pass is
 // built to wait for one batch of loads: an interaction loads its whole block (the TIR step of
 // each taken branch is pre-folded into the block's TM rows, wgrt_common.h kJ*), the two
-// candidate moves, and issues the cell-word loads of both candidate next positions and of the
-// position one hop beyond each; a miss hop only moves (its phase steps are applied as a power
-// at the next interaction) and issues the cell load two hops ahead.  JLane::pf / pf2 always
-// hold the cell words of the ray's position and of the position one hop further.  Out-coupled
+// candidate moves, and issues the cell-word loads of both candidate next positions; a miss hop
+// only moves (its phase steps are applied as a power at the next interaction) and issues the
+// cell load of its new position, read in the next pass (JLane::pf).  Out-coupled
 // rays are queued (position + ray index) and binned into matrix_EB by the epilogue kernel, so
 // the eyebox predicate and its divisions stay out of the wave loop.
 struct JRay {
@@ -683,7 +695,7 @@ struct JLane {
     const double *T;         // this ray's Jones tile
     int64_t i;
     uint32_t bounces;
-    uint64_t pf, pf2;        // locator cell words of (x, y) and (x + gx, y + gy)
+    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
 
 enum : int { kUncertain = -3 };
@@ -721,7 +733,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.s = A.rng[ld];
     L.r.region = 0;
     L.bounces = 1;
-    L.pf = L.pf2 = 0ull;
+    L.pf = 0ull;
     return true;
 }
 
@@ -804,7 +816,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double xa = r.x + mva.x, ya = r.y + mva.y;
     const double xb = r.x + mvb.x, yb = r.y + mvb.y;
     const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
-    const uint64_t pa2 = locate_c(loc, xa + mva.x, ya + mva.y), pb2 = locate_c(loc, xb + mvb.x, yb + mvb.y);
 
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     for (uint32_t h = 0; h < r.hops; ++h) {
@@ -884,7 +895,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.gx = ba ? mva.x : mvb.x;
     r.gy = ba ? mva.y : mvb.y;
     L.pf = ba ? pa : pb;
-    L.pf2 = ba ? pa2 : pb2;
     if (kind == 0) {
         DIAG_REGION(5);
         const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
@@ -896,8 +906,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 }
 
 // Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
-// that need no Monte-Carlo interaction, at most A.max_hops per call.  Every iteration tests
-// the cell word loaded at least one step earlier (L.pf) and issues the load two hops ahead.
+// that need no Monte-Carlo interaction, at most A.max_hops per call (1 by default: every
+// iteration then tests a cell word loaded a pass earlier, L.pf, and a hop issues the load of
+// the next one).
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     JRay &r = L.r;
@@ -930,8 +941,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         r.x = r.x + r.gx;
         r.y = r.y + r.gy;
         ++r.hops;
-        L.pf = L.pf2;
-        L.pf2 = locate_c(loc, r.x + r.gx, r.y + r.gy);
+        L.pf = locate_c(loc, r.x, r.y);   // used from the next pass on
     }
 }
 
@@ -1026,24 +1036,36 @@ __device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int
     return true;
 }
 
-// Runs right behind every Jones-vector launch on its stream: bins the queued out-couplings
-// into matrix_EB, and re-traces the rays the launch abandoned (uncertain decisions; nothing of
-// them was written) from their launch-start state with the reference arithmetic.  Usually the
-// replay list is empty.
-__global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
-    const unsigned long long nr = *A.replay_count;
-    const unsigned long long stride = (unsigned long long)gridDim.x * blockDim.x;
-    uint64_t b = 0, h = 0, bad = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_rays; i += (int64_t)stride) {
+// Runs right behind every Jones-vector launch on its stream: bins the recorded out-couplings
+// (ray i out-coupled this launch iff eb_tag[i] == epoch) into matrix_EB.
+__global__ __launch_bounds__(256) void eyebox_kernel(TraceArgs A) {
+    uint64_t h = 0;
+    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_rays;
+         i += (int64_t)gridDim.x * blockDim.x) {
         if (A.eb_tag[i] != A.epoch) continue;
+#ifdef WGRT_ABL_EBSCAN
+        h += 1;   // ablation build only: scan the tags, bin nothing
+#else
         const double2 p = A.eb_xy[i];
         const int m = (int)A.m[i], n = (int)A.n[i], l = A.l ? (int)A.l[i] : 0;
         h += eyebox_add(A, l, m, n, p.x, p.y);
+#endif
     }
-    for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr; k += stride)
+    add_stats(A.stats, 0, h, 0);
+}
+
+// Then re-traces the rays the launch abandoned (uncertain decisions; nothing of them was
+// written) from their launch-start state with the reference arithmetic.  Usually the list is
+// empty and every workgroup exits at once.
+__global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
+    const unsigned long long nr = *A.replay_count;
+    if ((unsigned long long)blockIdx.x * blockDim.x >= nr) return;   // workgroup-uniform
+    uint64_t b = 0, h = 0, bad = 0;
+    for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr;
+         k += (unsigned long long)gridDim.x * blockDim.x)
         trace_one(A, (int64_t)A.replay_list[k], b, h, bad);
     add_stats(A.stats, b, h, bad);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats && nr)
+    if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats)
         atomicAdd((unsigned long long *)&A.stats->replayed, nr);
 }
 
@@ -1056,10 +1078,44 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
 // `chunk` consecutive rays from the global counter when the chunk runs dry, and (3) runs
 // the fp64 interaction math for all lanes together.  Results are identical to variant 1:
 // each ray's evolution depends only on its own state and its global index.
+// Work queue of the Jones-vector variants: one head per XCD (each on its own 128-B line), head
+// x handing out chunks [x n / 8, (x + 1) n / 8) in order, so a die's waves share one stretch
+// of consecutive chunks (FoV x wavelength tiles stay in that XCD's L2) and the dequeue
+// atomics spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The
+// XCD id steers placement only: any wave may take any chunk, so correctness never depends on it.
+constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
+constexpr int kHeads = 8;
+constexpr int kScratchCtr = (kHeads + 1) * kHeadStride;   // heads + replay count
+
+__device__ __forceinline__ int xcc_id() {
+    unsigned v;
+    asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
+    return (int)(v & 7u);
+}
+
+// Next chunk for the calling wave (wave-uniform), or -1 when every head is exhausted.
+__device__ __forceinline__ int64_t pop_chunk_xcd(unsigned long long *heads, int &h, int64_t n_chunks, int lane) {
+    for (int tries = 0; tries < kHeads; ++tries) {
+        const int x = (h + tries) & (kHeads - 1);
+        const int64_t lo = n_chunks * x / kHeads, hi = n_chunks * (x + 1) / kHeads;
+        unsigned long long q = 0;
+        if (lane == 0) q = atomicAdd(heads + kHeadStride * x, 1ull);
+        q = __shfl(q, 0);
+        if (lo + (int64_t)q < hi) {
+            h = x;
+            return lo + (int64_t)q;
+        }
+    }
+    return -1;
+}
+
 template <class LaneT, class Loc>
 __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &loc, unsigned long long *counter,
-                                                int chunk) {
+                                                int chunk, bool xcd_heads = false) {
     const int lane = threadIdx.x & 63;
+    int head = xcd_heads ? xcc_id() : 0;
+    int pend_h = -1;                  // head of the dequeue in flight (-1: none)
+    unsigned long long pend_v = 0;    // its result (lane 0)
     const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     int64_t cur = 0, end = 0;  // wave-uniform chunk cursor
     bool exhausted = false;
@@ -1078,6 +1134,9 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
 #endif
 #ifdef WGRT_PHASES
     uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+#ifdef WGRT_PHASES_DRAIN
+    uint64_t ph_drain[2] = {0, 0};
+#endif
     const int p_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1085,6 +1144,11 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
 #ifdef WGRT_PHASES
         const uint64_t pt0 = __builtin_amdgcn_s_memtime();
         const int pofs = exhausted ? 4 : 0;
+#ifdef WGRT_PHASES_DRAIN
+        // diagnostic: drain everything the previous pass left in flight, timed on its own
+        __builtin_amdgcn_s_waitcnt(0);
+        ph_drain[exhausted ? 1 : 0] += __builtin_amdgcn_s_memtime() - pt0;
+#endif
 #endif
         if (active) {
 #ifdef WGRT_DIAG
@@ -1120,8 +1184,28 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
                     q = w + W * (unsigned long long)(d_static_k++);
                 }
 #else
-                if (lane == 0) q = atomicAdd(counter, 1ull);
-                q = __shfl(q, 0);
+                const int64_t n_chunks_ = (A.n_rays + chunk - 1) / chunk;
+                if (xcd_heads) {
+                    // the dequeue for this chunk was issued when the previous one started
+                    // (pend_v, on head pend_h): its latency overlapped that chunk's passes
+                    int64_t c = -1;
+                    if (pend_h >= 0) {
+                        const unsigned long long pq = __shfl(pend_v, 0);
+                        const int64_t lo = n_chunks_ * pend_h / kHeads, hi = n_chunks_ * (pend_h + 1) / kHeads;
+                        if (lo + (int64_t)pq < hi) c = lo + (int64_t)pq;
+                        else head = (pend_h + 1) & (kHeads - 1);   // that head ran dry: move on
+                    }
+                    if (c < 0) c = pop_chunk_xcd(counter, head, n_chunks_, lane);
+                    q = c < 0 ? (unsigned long long)n_chunks_ : (unsigned long long)c;
+                    pend_h = -1;
+                    if (c >= 0) {   // issue the next dequeue now; it is read when this chunk runs dry
+                        pend_h = head;
+                        if (lane == 0) pend_v = atomicAdd(counter + kHeadStride * head, 1ull);
+                    }
+                } else {
+                    if (lane == 0) q = atomicAdd(counter, 1ull);
+                    q = __shfl(q, 0);
+                }
 #endif
                 const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
                 if ((int64_t)q >= n_chunks) {
@@ -1161,6 +1245,11 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
             need = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
+#ifdef WGRT_AGE_PRIO
+        // experiment: issue priority for waves carrying old (long-lived) rays
+        if (__ballot(active && L.bounces > (uint32_t)WGRT_AGE_PRIO) != 0ull) __builtin_amdgcn_s_setprio(2);
+        else __builtin_amdgcn_s_setprio(0);
+#endif
 #ifdef WGRT_PHASES
         const uint64_t pt2 = __builtin_amdgcn_s_memtime();
 #endif
@@ -1203,6 +1292,10 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
 #ifdef WGRT_PHASES
     if (lane == 0) {
         for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
+#ifdef WGRT_PHASES_DRAIN
+        atomicAdd(&g_phase[11], (unsigned long long)ph_drain[0]);
+        atomicAdd(&g_phase[12], (unsigned long long)ph_drain[1]);
+#endif
         if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
@@ -1241,7 +1334,7 @@ __global__ __launch_bounds__(256, W) void trace_persistent_g_kernel(TraceArgs A,
 template <class CellT, int W>
 __global__ __launch_bounds__(256, W) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    persistent_body<JLane>(A, loc, counter, chunk);
+    persistent_body<JLane>(A, loc, counter, chunk, true);
 }
 
 // Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
@@ -1374,7 +1467,7 @@ struct wgrt_scene {
     // Jones-vector launches: per-stream work counter + replay list (launches on one stream are
     // ordered, so they may share; launches on different streams never do)
     struct Scratch {
-        unsigned long long *ctr = nullptr;   // [0] chunk counter, [1] replay count
+        unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), then the replay count
         uint32_t *list = nullptr;            // replay list
         double2 *eb_xy = nullptr;            // out-couplings by ray: position, launch tag
         uint32_t *eb_tag = nullptr;
@@ -1621,7 +1714,7 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
             std::lock_guard<std::mutex> lk(ms->scratch_mu);
             sc = &ms->scratch[stream];
             if (!sc->ctr) {
-                hipError_t e = hipMalloc((void **)&sc->ctr, 2 * sizeof(unsigned long long));
+                hipError_t e = hipMalloc((void **)&sc->ctr, kScratchCtr * sizeof(unsigned long long));
                 if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
             }
             if (sc->cap < n_rays) {
@@ -1643,7 +1736,7 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
                 sc->cap = n_rays;
             }
         }
-        A.replay_count = sc->ctr + 1;
+        A.replay_count = sc->ctr + kHeads * kHeadStride;
         A.replay_list = sc->list;
         if (++sc->epoch == 0) {   // tags wrapped (after 2^32 launches): clear them
             HIP_TRY(hipMemsetAsync(sc->eb_tag, 0, (size_t)sc->cap * sizeof(uint32_t), st));
@@ -1652,7 +1745,9 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         A.eb_xy = sc->eb_xy;
         A.eb_tag = sc->eb_tag;
         A.epoch = sc->epoch;
-        HIP_TRY(hipMemsetAsync(sc->ctr, 0, 2 * sizeof(unsigned long long), st));
+        HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
+        const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
+        A.max_hops = g_jmax_hops;
         int64_t grid = workgroups > 0 ? workgroups
                                       : (variant == 7 ? s->jones_grid : variant == 8 ? s->jones_w4_grid : s->jones64_grid);
         const int64_t useful = (n_rays + 255) / 256;
@@ -1666,16 +1761,18 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
         if (variant == 7)
             hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
-                               sc->ctr, kChunk);
+                               sc->ctr, jchunk);
         else if (variant == 8)
             hipLaunchKernelGGL((trace_jones_kernel<uint32_t, WGRT_W8>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
-                               sc->ctr, kChunk);
+                               sc->ctr, jchunk);
         else
             hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, A.loc,
-                               sc->ctr, kChunk);
+                               sc->ctr, jchunk);
         HIP_TRY(hipGetLastError());
         const int64_t eblocks = std::min<int64_t>((n_rays + 255) / 256, 2048);
-        hipLaunchKernelGGL(epilogue_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
+        hipLaunchKernelGGL(eyebox_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
+        HIP_TRY(hipGetLastError());
+        hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
     } else if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
         if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");

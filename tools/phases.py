@@ -55,6 +55,8 @@ for tag, o in (("before dry", 0), ("after dry ", 4)):
     tot = p[o] + p[o + 1] + p[o + 2]
     print(f"{tag}: passes={p[o + 3]} cycles/pass advance={p[o] / n:.0f} refill={p[o + 1] / n:.0f} "
           f"interact={p[o + 2] / n:.0f} total={tot / n:.0f}")
+if p[11] or p[12]:
+    print(f"drain at pass start (cycles/pass): before dry {p[11] / max(p[3], 1):.0f}, after dry {p[12] / max(p[7], 1):.0f}")
 w = np.array(wt, dtype=np.float64).reshape(-1, 3)
 w = w[w[:, 0] > 0]
 t0 = w[:, 0].min()
