@@ -60,7 +60,8 @@ class TraceStats(ctypes.Structure):
 
 class LaunchOpts(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_int), ("variant", ctypes.c_int), ("workgroups", ctypes.c_int),
-                ("chunk_order", ctypes.c_void_p), ("n_chunk_order", ctypes.c_int64)]
+                ("chunk_order", ctypes.c_void_p), ("n_chunk_order", ctypes.c_int64),
+                ("num_iter", ctypes.c_int)]
 
 
 class SceneInfo(ctypes.Structure):

@@ -104,8 +104,8 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
         xmax = ymax = 1.0;
     }
     double h = cell_mm;
-    // keep the grid below ~16M cells (128 MB of 64-bit words) whatever the coordinate range
-    while (((xmax - xmin) / h + 5) * ((ymax - ymin) / h + 5) > 1.6e7) h *= 2.0;
+    // keep the grid below ~32M cells (256 MB of 64-bit host words) whatever the coordinate range
+    while (((xmax - xmin) / h + 5) * ((ymax - ymin) / h + 5) > 3.2e7) h *= 2.0;
     const double x0 = std::floor(xmin / h) * h - 2 * h;
     const double y0 = std::floor(ymin / h) * h - 2 * h;
     const int ncx = (int)std::ceil((xmax - x0) / h) + 3;
@@ -133,6 +133,28 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
                 if (!(ey1 < by0 || ey0 > by1)) out.row_edges.push_back((int32_t)i);
             }
             out.row_off[(size_t)k * ncy + cy + 1] = (int32_t)out.row_edges.size();
+        }
+    }
+    out.bands.assign((size_t)np * ncy * 4 * kBandSegs, NAN);
+    for (int k = 0; k < np; ++k) {
+        const double *xy = polys[k];
+        const int64_t nv = nverts[k];
+        for (int cy = 0; cy < ncy; ++cy) {
+            const size_t r = (size_t)k * ncy + cy;
+            double *rec = out.bands.data() + r * 4 * kBandSegs;
+            const int e0 = out.row_off[r], e1 = out.row_off[r + 1];
+            if (e1 - e0 > kBandSegs) {
+                rec[0] = INFINITY;
+                continue;
+            }
+            for (int e = e0; e < e1; ++e) {
+                const int64_t i = out.row_edges[e], j = (i == 0) ? nv - 1 : i - 1;
+                double *sg = rec + 4 * (e - e0);
+                sg[0] = xy[2 * j];
+                sg[1] = xy[2 * j + 1];
+                sg[2] = xy[2 * i];
+                sg[3] = xy[2 * i + 1];
+            }
         }
     }
     std::vector<double> xs;

@@ -8,6 +8,8 @@
 
 namespace wgrt {
 
+constexpr int kBandSegs = 4;
+
 struct LocatorHost {
     std::vector<uint64_t> cells;   // [ncy][ncx], 2 bits per polygon: 0 OUT, 1 IN, 2 EDGE
     std::vector<double> verts;     // all polygon vertices, [V][2]
@@ -17,6 +19,11 @@ struct LocatorHost {
     // as the index i (within polygon k) of its end vertex; its start vertex is i - 1 (mod nv)
     std::vector<int32_t> row_off;
     std::vector<int32_t> row_edges;
+    // the same row bands as fixed 128-B records (Jones-vector kernels): up to kBandSegs
+    // segments (x_start, y_start, x_end, y_end) of polygon k's edges meeting row cy, unused
+    // slots NaN (inert in the predicate); a band with more edges starts with +inf and is
+    // resolved through row_off / row_edges instead
+    std::vector<double> bands;
     double x0 = 0, y0 = 0, h = 0, inv_h = 0;
     int ncx = 0, ncy = 0;
     int64_t edge_cells = 0;

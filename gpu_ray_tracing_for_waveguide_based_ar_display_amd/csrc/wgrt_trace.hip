@@ -103,6 +103,7 @@ struct LocatorT {
     const int32_t *row_edges;
     double x0, y0, inv_h;
     int ncx, ncy;
+    const double *bands;    // 128-B band records (LocatorHost::bands); NULL: CSR lists only
 };
 using Locator = LocatorT<uint64_t>;
 
@@ -140,6 +141,11 @@ struct TraceArgs {
     double cert_tol;   // Jones-vector variants: base of the decision certification bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
+    // fused launches (variants 7-9, n_iter > 1): n_iter chained traces of every ray in one
+    // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
+    int n_iter;
+    uint64_t *rng64;
+    uint32_t iter_epoch;
 };
 
 constexpr int kPolyEff1 = 0;
@@ -182,6 +188,11 @@ __device__ __forceinline__ void diag_region(int r) {
 #define DIAG_REGION(r) diag_region(r)
 #else
 #define DIAG_REGION(r) ((void)0)
+#endif
+#ifdef WGRT_ASM_MARKS
+#define ASM_MARK(t) asm volatile(";#MARK " t)
+#else
+#define ASM_MARK(t) ((void)0)
 #endif
 
 // A point's cell of the locator grid: the per-polygon class word and the cell row.
@@ -254,8 +265,23 @@ __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, in
 #endif
     DIAG_REGION(4);
     const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
-    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
     const int r = k * L.ncy + cy;
+    // one 128-B record: the (at most kBandSegs) edges of polygon k meeting this cell row,
+    // evaluated with the reference predicate's operations (GRTF:36-71); NaN slots are inert
+    const double4 *rec = (const double4 *)(L.bands + (size_t)r * 4 * kBandSegs);
+    const double4 s0 = rec[0], s1 = rec[1], s2 = rec[2], s3 = rec[3];
+    if (s0.x != INFINITY) {
+        bool inside = false;
+        const double4 sg[kBandSegs] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int e = 0; e < kBandSegs; ++e) {
+            const double xj = sg[e].x, yj = sg[e].y, xi = sg[e].z, yi = sg[e].w;
+            if (on_segment(x, y, xj, yj, xi, yi)) return true;
+            if (((yi > y) != (yj > y)) && (x < (xj - xi) * (y - yi) / (yj - yi + 1e-20) + xi)) inside = !inside;
+        }
+        return inside;
+    }
+    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
     const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
     return inside_or_on_edge_subset(x, y, L.verts + 2 * a, nv, L.row_edges + e0, e1 - e0);
 }
@@ -647,6 +673,25 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     }
 }
 
+// Eyebox accumulation of an out-coupling (GRTF:1162-1171, 1231-1240): the per-FoV
+// eyebox rectangle test, the bin, and the atomic; compiled-numba addressing as in interact().
+__device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int n, double x, double y) {
+    const double *T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
+    if (!inside_or_on_edge(x, y, T + kTileEbRect, 4)) return false;
+    const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
+    const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
+    const double dx = (xmax - xmin) / kEbNx, dy = (ymax - ymin) / kEbNy;
+    int64_t ix = (int64_t)floor((x - xmin) / dx);
+    int64_t iy = (int64_t)floor((y - ymin) / dy);
+    if (ix < 0) ix += kEbNx;
+    if (iy < 0) iy += kEbNy;
+    const int64_t off = ((((int64_t)l * A.ny + n) * A.nx + m) * kEbNy + iy) * kEbNx + ix;
+    const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
+    if (off < 0 || off >= total) return false;
+    unsafeAtomicAdd(A.eb + off, 1.0f);
+    return true;
+}
+
 // ----------------------------------------------------------------------------
 // Jones-vector path (variants 7-9): certified decisions, side-effect-free abandon + replay
 // ----------------------------------------------------------------------------
@@ -695,6 +740,9 @@ struct JLane {
     const double *T;         // this ray's Jones tile
     int64_t i;
     uint32_t bounces;
+    uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
+    uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
+    bool hit;                // fused launches: accumulated into matrix_EB
     uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
 
@@ -733,6 +781,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.s = A.rng[ld];
     L.r.region = 0;
     L.bounces = 1;
+    L.hit = false;
     L.pf = 0ull;
     return true;
 }
@@ -793,13 +842,14 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
 // Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
 // kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
 // of it has been written) and replayed.
-template <class Loc>
+template <bool FUSED = false, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
                                         bool entry) {
     JRay &r = L.r;
     const double *T = L.T;
     const double *B = T + kJHeader + kJBlock * blk;
     DIAG_REGION(0);
+    ASM_MARK("interact-begin");
     const bool three = kind >= 3;
     const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
     // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
@@ -817,6 +867,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double xb = r.x + mvb.x, yb = r.y + mvb.y;
     const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
 
+    ASM_MARK("interact-hoploop");
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     for (uint32_t h = 0; h < r.hops; ++h) {
         const double mr = r.mr;
@@ -824,6 +875,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
         r.mi = fma(mr, hop.y, r.mi * hop.x);
     }
     r.hops = 0;
+    ASM_MARK("interact-math");
     const double denom = entry ? cg.x : r.cos_t;
     const double u = rng_draw(r.s, A.gid_offset + L.i);
     const JField f0 = jones(k0, r), f1 = jones(k1, r);
@@ -862,6 +914,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
                  (!three || u > c2 || fabs(g2 - t) > m2);
         }
     }
+    ASM_MARK("interact-decide");
     if (!ok) return kUncertain;
     int b;
     if (u <= c0 && p0) b = 0;
@@ -869,13 +922,20 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     else if (three && u <= c2 && p2) b = 2;
     else return kDie;
 
-    if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240): recorded for the epilogue
+    if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
         DIAG_REGION(2);
-        A.eb_xy[L.i] = double2{r.x, r.y};
-        A.eb_tag[L.i] = A.epoch;
+        if (FUSED) {   // several traces of a ray per launch: bin now
+            const int64_t g = (int64_t)((double)(T - A.jtiles) / (double)A.jtile_d);   // exact: < 2^40
+            const int n = (int)(g % A.ny), m = (int)((g / A.ny) % A.nx), l = (int)(g / ((int64_t)A.ny * A.nx));
+            L.hit = eyebox_add(A, l, m, n, r.x, r.y);
+        } else {       // recorded; eyebox_kernel bins it after the launch
+            A.eb_xy[L.i] = double2{r.x, r.y};
+            A.eb_tag[L.i] = A.epoch;
+        }
         return kDie;
     }
     DIAG_REGION(1);
+    ASM_MARK("interact-take");
     const bool ba = b == 0;
     const JField f = ba ? f0 : f1;
     const double n2 = ba ? q0 : q1;
@@ -895,6 +955,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.gx = ba ? mva.x : mvb.x;
     r.gy = ba ? mva.y : mvb.y;
     L.pf = ba ? pa : pb;
+    ASM_MARK("interact-take-end");
     if (kind == 0) {
         DIAG_REGION(5);
         const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
@@ -976,13 +1037,17 @@ __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t boun
     }
 }
 
-// Trace ray i to termination with the reference arithmetic (variant 1's lane; replays).
-__device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad) {
+// Trace ray i to termination with the reference arithmetic (variant 1's lane; replays).  With
+// s_io, the trace starts from *s_io instead of rng_states[i] and leaves its final state there
+// (rng_states untouched).
+__device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad,
+                                          uint32_t *s_io = nullptr) {
     Lane L;
     if (!lane_load(A, i, L)) {
         ++bad;
         return;
     }
+    if (s_io) L.r.s = *s_io;
     int blk = 0, kind = 0;
     bool entry = true;
     for (;;) {
@@ -1001,7 +1066,8 @@ __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_
 #endif
         if (blk < 0) break;
     }
-    lane_retire(A, L);
+    if (s_io) *s_io = L.r.s;
+    else lane_retire(A, L);
     b += L.bounces;
     h += L.hit;
 #ifdef WGRT_TIMERS
@@ -1015,25 +1081,6 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     uint64_t b = 0, h = 0, bad = 0;
     if (i < A.n_rays) trace_one(A, i, b, h, bad);
     add_stats(A.stats, b, h, bad);
-}
-
-// Eyebox accumulation of a queued out-coupling (GRTF:1162-1171, 1231-1240): the per-FoV
-// eyebox rectangle test, the bin, and the atomic; compiled-numba addressing as in interact().
-__device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int n, double x, double y) {
-    const double *T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
-    if (!inside_or_on_edge(x, y, T + kTileEbRect, 4)) return false;
-    const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
-    const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
-    const double dx = (xmax - xmin) / kEbNx, dy = (ymax - ymin) / kEbNy;
-    int64_t ix = (int64_t)floor((x - xmin) / dx);
-    int64_t iy = (int64_t)floor((y - ymin) / dy);
-    if (ix < 0) ix += kEbNx;
-    if (iy < 0) iy += kEbNy;
-    const int64_t off = ((((int64_t)l * A.ny + n) * A.nx + m) * kEbNy + iy) * kEbNx + ix;
-    const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
-    if (off < 0 || off >= total) return false;
-    unsafeAtomicAdd(A.eb + off, 1.0f);
-    return true;
 }
 
 // Runs right behind every Jones-vector launch on its stream: bins the recorded out-couplings
@@ -1062,8 +1109,17 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
     if ((unsigned long long)blockIdx.x * blockDim.x >= nr) return;   // workgroup-uniform
     uint64_t b = 0, h = 0, bad = 0;
     for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr;
-         k += (unsigned long long)gridDim.x * blockDim.x)
-        trace_one(A, (int64_t)A.replay_list[k], b, h, bad);
+         k += (unsigned long long)gridDim.x * blockDim.x) {
+        const int64_t i = (int64_t)A.replay_list[k];
+        if (A.n_iter <= 1) {
+            trace_one(A, i, b, h, bad);
+        } else {   // fused launch: the traces from the abandoned one to the last, chained
+            const uint64_t w = A.rng64[i];
+            uint32_t st = (uint32_t)(w >> 32);
+            for (int it = (int)(w & 0xffu); it < A.n_iter; ++it) trace_one(A, i, b, h, bad, &st);
+            A.rng[i] = st;
+        }
+    }
     add_stats(A.stats, b, h, bad);
     if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats)
         atomicAdd((unsigned long long *)&A.stats->replayed, nr);
@@ -1110,8 +1166,10 @@ __device__ __forceinline__ int64_t pop_chunk_xcd(unsigned long long *heads, int 
 }
 
 template <class LaneT, class Loc>
-__device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &loc, unsigned long long *counter,
+__device__ __forceinline__ void persistent_body(const TraceArgs &A0, const Loc &loc0, unsigned long long *counter,
                                                 int chunk, bool xcd_heads = false) {
+    const TraceArgs &A = A0;
+    const Loc &loc = loc0;
     const int lane = threadIdx.x & 63;
     int head = xcd_heads ? xcc_id() : 0;
     int pend_h = -1;                  // head of the dequeue in flight (-1: none)
@@ -1299,7 +1357,7 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A, const Loc &l
         if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
     }
 #endif
-    add_stats(A.stats, tot_b, tot_h, tot_bad);
+    add_stats(A0.stats, tot_b, tot_h, tot_bad);
 #ifdef WGRT_DIAG
     if (lane == 0) {
         if (d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 2] = __builtin_amdgcn_s_memrealtime();
@@ -1329,12 +1387,171 @@ __global__ __launch_bounds__(256, W) void trace_persistent_g_kernel(TraceArgs A,
     persistent_body<Lane>(A, loc, counter, chunk);
 }
 
+// Tag of a fused launch's per-ray RNG word: launch epoch, broken flag, traces completed.
+__device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool broken) {
+    return (epoch << 9) | (broken ? 0x100u : 0u) | k;
+}
+
+// The persistent loop of the Jones-vector variants.  Work items are 64-ray chunks handed out
+// by the per-XCD heads.  FUSED: a launch runs A.n_iter chained traces of every ray (the
+// reference's num_iter loop of launches, MAIN:169-177, each starting from the RNG state the
+// previous one left): head x hands out (iteration, chunk) items iteration-major, so one
+// iteration's drain overlaps the next one's bulk.  A trace of iteration k >= 1 may start only
+// once the ray's trace k - 1 has ended: its end writes the 8-byte granule {state, tag} with an
+// agent-scope store, and a lane that takes the ray polls that granule with agent-scope loads
+// (waiting in place, lane idle, until the tag says k) -- the granule hand-off of
+// MI355X_MICROARCH.md's price list, valid whatever the XCD placement.  Results are identical
+// to n_iter launches: each ray's traces run in order from the same states; eyebox adds commute.
+template <bool FUSED, class Loc>
+__device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, unsigned long long *heads, int chunk) {
+    const int lane = threadIdx.x & 63;
+    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
+    const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
+    const int64_t n_iter = FUSED ? A.n_iter : 1;
+    int head = xcc_id();
+    int pend_h = -1;                  // head of the dequeue in flight (-1: none)
+    unsigned long long pend_v = 0;    // its result (lane 0)
+    int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
+    uint32_t cur_k = 0;               // the item's iteration
+    bool exhausted = false;
+    bool active = false, waiting = false;
+    JLane L;
+    int blk = 0, kind = 0;
+    bool entry = false;
+    uint32_t tot_b = 0, tot_h = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
+
+    // head x's items: iteration-major over its chunk range [lo, hi)
+    auto decode = [&](int x, int64_t q, int64_t &c, uint32_t &k) -> bool {
+        const int64_t lo = n_chunks * x / kHeads, hi = n_chunks * (x + 1) / kHeads, cx = hi - lo;
+        if (cx <= 0 || q >= cx * n_iter) return false;
+        k = (uint32_t)(q / cx);
+        c = lo + q % cx;
+        return true;
+    };
+    // start the trace (L.i, L.k) on this lane: active, waiting (previous trace still running) or
+    // skipped (bad ray / ray already handed to the replay)
+    auto start = [&]() {
+        const bool ok = lane_load(A, L.i, L);
+        waiting = false;
+        active = false;
+        if (!ok) {
+            ++tot_bad;
+            return;
+        }
+        if (FUSED && L.k > 0) {
+            const uint64_t w = __hip_atomic_load(A.rng64 + L.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t tag = (uint32_t)w;
+            if (tag == iter_tag(A.iter_epoch, L.k, false)) {
+                L.r.s = (uint32_t)(w >> 32);
+            } else if ((tag >> 8) == ((A.iter_epoch << 1) | 1u)) {
+                return;   // abandoned in an earlier iteration: the replay kernel finishes it
+            } else {
+                waiting = true;
+                return;
+            }
+        }
+        L.s0 = L.r.s;
+        active = true;
+        blk = 0;
+        kind = 0;
+        entry = true;
+    };
+    auto retire = [&]() {
+        tot_b += L.bounces;
+        tot_h += L.hit;
+        if (FUSED && (int64_t)L.k + 1 < n_iter) {
+            __hip_atomic_store(A.rng64 + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
+                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        } else {
+            A.rng[L.i] = L.r.s;
+            if (!FUSED && A.per_ray) A.per_ray[L.i] = L.bounces;
+        }
+        active = false;
+    };
+
+    for (;;) {
+        if (active) {
+            blk = advance(A, loc, L, kind);
+            entry = false;
+            if (blk == kDie) retire();
+        }
+        if (FUSED && waiting) start();   // poll the previous trace's granule again
+        uint64_t need = __ballot(!active && !waiting);
+        while (need != 0ull && !exhausted) {
+            if (cur >= end) {
+                // the dequeue for this item was issued when the previous one started (pend_v,
+                // on head pend_h): its latency overlapped that item's passes
+                int64_t c = -1;
+                uint32_t k = 0;
+                bool got = false;
+                if (pend_h >= 0) {
+                    const unsigned long long pq = __shfl(pend_v, 0);
+                    got = decode(pend_h, (int64_t)pq, c, k);
+                    if (!got) head = (pend_h + 1) & (kHeads - 1);   // that head ran dry: move on
+                }
+                for (int tries = 0; !got && tries < kHeads; ++tries) {
+                    const int x = (head + tries) & (kHeads - 1);
+                    unsigned long long q = 0;
+                    if (lane == 0) q = atomicAdd(heads + kHeadStride * x, 1ull);
+                    q = __shfl(q, 0);
+                    if (decode(x, (int64_t)q, c, k)) {
+                        head = x;
+                        got = true;
+                    }
+                }
+                pend_h = -1;
+                if (!got) {
+                    exhausted = true;
+                    break;
+                }
+                pend_h = head;   // issue the next dequeue now; read when this item runs dry
+                if (lane == 0) pend_v = atomicAdd(heads + kHeadStride * head, 1ull);
+                const int64_t cc = (!FUSED && A.order) ? (int64_t)A.order[c] : c;
+                cur = cc * chunk;
+                end = cur + chunk < A.n_rays ? cur + chunk : A.n_rays;
+                cur_k = k;
+            }
+            const int want = __popcll(need);
+            const int64_t avail = end - cur;
+            const int take = (int64_t)want < avail ? want : (int)avail;
+            if (!active && !waiting) {
+                const int rank = __popcll(need & lt_mask);
+                if (rank < take) {
+                    L.i = cur + rank;
+                    L.k = cur_k;
+                    start();
+                }
+            }
+            cur += take;
+            need = __ballot(!active && !waiting);
+        }
+        if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
+        if (active && blk >= 0) {
+            const int next = interact<FUSED>(A, loc, L, blk, kind, entry);
+            if (next == kUncertain) {
+                // abandoned with no side effect; replay_kernel re-traces it (fused: from this
+                // iteration on, so later iterations skip the ray)
+                if (FUSED)
+                    __hip_atomic_store(A.rng64 + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                A.replay_list[atomicAdd(A.replay_count, 1ull)] = (uint32_t)L.i;
+                active = false;
+            } else if (next < 0) {
+                retire();
+            } else {
+                L.r.region = next;
+            }
+        }
+    }
+    add_stats(A.stats, tot_b, tot_h, tot_bad);
+}
+
 // Variants 7-9: the persistent loop over the Jones-vector path (32-bit cell words at W waves
 // per SIMD; 64-bit cell words for scenes of more than 16 polygons).
-template <class CellT, int W>
+template <class CellT, int W, bool FUSED = false>
 __global__ __launch_bounds__(256, W) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    persistent_body<JLane>(A, loc, counter, chunk, true);
+    jones_body<FUSED>(A, loc, counter, chunk);
 }
 
 // Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
@@ -1357,6 +1574,7 @@ __global__ __launch_bounds__(768, 1) void trace_persistent_lds_kernel(TraceArgs 
     loc.poly_off = (const int32_t *)(smem + D.off_poly);
     loc.row_off = (const int32_t *)(smem + D.off_row_off);
     loc.row_edges = (const int32_t *)(smem + D.off_row_edges);
+    loc.bands = nullptr;
     loc.x0 = D.x0;
     loc.y0 = D.y0;
     loc.inv_h = D.inv_h;
@@ -1371,10 +1589,15 @@ __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, con
     if (i >= n) return;
     const double x = xy[2 * i], y = xy[2 * i + 1];
     const Cell w = locate(L, x, y);
-    uint64_t mask = 0;
-    for (int k = 0; k < npoly; ++k)
-        if (in_poly(L, w, k, x, y)) mask |= 1ull << k;
-    out[i] = mask;
+    const uint64_t ww = locate_w(L, x, y);
+    uint64_t mask = 0, mism = 0;
+    for (int k = 0; k < npoly; ++k) {
+        const bool a = in_poly(L, w, k, x, y);      // CSR row lists (variants 1-6)
+        const bool b = in_poly_w(L, ww, k, x, y);   // 128-B band records (variants 7-9)
+        if (a) mask |= 1ull << k;
+        if (a != b) mism = 1ull << 63;
+    }
+    out[i] = mask | mism;
 }
 
 // Ray setup of FoV x wavelength blocks [blk_lo, blk_lo + n / R) (reference MAIN:65-115, 158):
@@ -1448,6 +1671,7 @@ struct wgrt_scene {
     int32_t *d_poly_off = nullptr;
     int32_t *d_row_off = nullptr;
     int32_t *d_row_edges = nullptr;
+    double *d_bands = nullptr;
     LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
     int64_t tiles = 0;
     // work counters of the persistent kernel: a ring, so launches in flight on different
@@ -1473,6 +1697,9 @@ struct wgrt_scene {
         uint32_t *eb_tag = nullptr;
         uint32_t epoch = 0;
         int64_t cap = 0;
+        uint64_t *rng64 = nullptr;           // fused launches: per-ray {state, tag} granules
+        uint32_t iter_epoch = 0;             // < 2^23 (iter_tag)
+        int64_t cap64 = 0;
     };
     std::mutex scratch_mu;
     std::map<void *, Scratch> scratch;
@@ -1487,6 +1714,7 @@ Locator make_locator(const wgrt_scene *s) {
     L.poly_off = s->d_poly_off;
     L.row_off = s->d_row_off;
     L.row_edges = s->d_row_edges;
+    L.bands = s->d_bands;
     L.x0 = s->loc_host.x0;
     L.y0 = s->loc_host.y0;
     L.inv_h = s->loc_host.inv_h;
@@ -1537,7 +1765,8 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         (st = upload(host.loc.verts, &s->d_verts)) != WGRT_OK ||
         (st = upload(host.loc.poly_off, &s->d_poly_off)) != WGRT_OK ||
         (st = upload(host.loc.row_off, &s->d_row_off)) != WGRT_OK ||
-        (st = upload(host.loc.row_edges, &s->d_row_edges)) != WGRT_OK) {
+        (st = upload(host.loc.row_edges, &s->d_row_edges)) != WGRT_OK ||
+        (st = upload(host.loc.bands, &s->d_bands)) != WGRT_OK) {
         wgrt_scene_destroy(s);
         return st;
     }
@@ -1597,6 +1826,8 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     s->loc_host.cells.shrink_to_fit();
     s->loc_host.row_edges.clear();
     s->loc_host.row_edges.shrink_to_fit();
+    s->loc_host.bands.clear();
+    s->loc_host.bands.shrink_to_fit();
     *out = s;
     return WGRT_OK;
 }
@@ -1613,12 +1844,14 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_counters);
     (void)hipFree(s->d_row_off);
     (void)hipFree(s->d_row_edges);
+    (void)hipFree(s->d_bands);
     (void)hipFree(s->d_lds_image);
     for (auto &kv : s->scratch) {
         (void)hipFree(kv.second.ctr);
         (void)hipFree(kv.second.list);
         (void)hipFree(kv.second.eb_xy);
         (void)hipFree(kv.second.eb_tag);
+        (void)hipFree(kv.second.rng64);
     }
     delete s;
     return WGRT_OK;
@@ -1646,7 +1879,8 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
 static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
                                 uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
                                 uint32_t *per_ray_bounces, void *stream, int variant, int workgroups, bool single,
-                                const int32_t *chunk_order = nullptr, int64_t n_chunk_order = 0) {
+                                const int32_t *chunk_order = nullptr, int64_t n_chunk_order = 0,
+                                int num_iter = 1) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
     if (single && s->nl != 1)
@@ -1661,6 +1895,18 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     if (variant >= 7 && n_rays > 0xffffffffll)
         return fail(WGRT_ERR_UNSUPPORTED, "variants 7-9 index at most 2^32 - 1 rays per launch");
     if (variant == 0) variant = s->d_cells32 ? 7 : (n_rays <= 0xffffffffll ? 9 : 2);   // auto
+    if (num_iter < 1) num_iter = 1;
+    if (num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter must be <= 255");
+    if (num_iter > 1 && (per_ray_bounces || chunk_order))
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter > 1 takes no per_ray_bounces / chunk_order");
+    if (num_iter > 1 && variant < 7) {   // chained launches, as the reference issues them
+        for (int it = 0; it < num_iter; ++it) {
+            const wgrt_status e = trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, nullptr,
+                                               stream, variant, workgroups, single);
+            if (e != WGRT_OK) return e;
+        }
+        return WGRT_OK;
+    }
     TraceArgs A;
     A.x = rays->x;
     A.y = rays->y;
@@ -1706,6 +1952,9 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.eb_xy = nullptr;
     A.eb_tag = nullptr;
     A.epoch = 0;
+    A.n_iter = 1;
+    A.rng64 = nullptr;
+    A.iter_epoch = 0;
     hipStream_t st = (hipStream_t)stream;
     if (variant >= 7) {
         wgrt_scene *ms = const_cast<wgrt_scene *>(s);
@@ -1735,6 +1984,27 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
                 if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
                 sc->cap = n_rays;
             }
+            if (num_iter > 1 && sc->cap64 < n_rays) {
+                HIP_TRY(hipStreamSynchronize(st));
+                (void)hipFree(sc->rng64);
+                sc->rng64 = nullptr;
+                sc->cap64 = 0;
+                sc->iter_epoch = 0;
+                hipError_t e = hipMalloc((void **)&sc->rng64, (size_t)n_rays * sizeof(uint64_t));
+                if (e == hipSuccess) e = hipMemset(sc->rng64, 0, (size_t)n_rays * sizeof(uint64_t));
+                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+                sc->cap64 = n_rays;
+            }
+        }
+        if (num_iter > 1) {
+            if (++sc->iter_epoch >= (1u << 23)) {   // granule tags wrapped: clear them
+                HIP_TRY(hipMemsetAsync(sc->rng64, 0, (size_t)sc->cap64 * sizeof(uint64_t), st));
+                sc->iter_epoch = 1;
+            }
+            A.n_iter = num_iter;
+            A.rng64 = sc->rng64;
+            A.iter_epoch = sc->iter_epoch;
         }
         A.replay_count = sc->ctr + kHeads * kHeadStride;
         A.replay_list = sc->list;
@@ -1758,8 +2028,16 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         l32.poly_off = A.loc.poly_off;
         l32.row_off = A.loc.row_off;
         l32.row_edges = A.loc.row_edges;
+        l32.bands = A.loc.bands;
         l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
-        if (variant == 7)
+        if (num_iter > 1) {
+            if (variant == 9)
+                hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3, true>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   A.loc, sc->ctr, jchunk);
+            else
+                hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3, true>), dim3((unsigned)grid), dim3(256), 0, st, A,
+                                   l32, sc->ctr, jchunk);
+        } else if (variant == 7)
             hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
                                sc->ctr, jchunk);
         else if (variant == 8)
@@ -1769,9 +2047,11 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
             hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, A.loc,
                                sc->ctr, jchunk);
         HIP_TRY(hipGetLastError());
-        const int64_t eblocks = std::min<int64_t>((n_rays + 255) / 256, 2048);
-        hipLaunchKernelGGL(eyebox_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
-        HIP_TRY(hipGetLastError());
+        if (num_iter == 1) {   // fused launches bin their out-couplings inline
+            const int64_t eblocks = std::min<int64_t>((n_rays + 255) / 256, 2048);
+            hipLaunchKernelGGL(eyebox_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
+            HIP_TRY(hipGetLastError());
+        }
         hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
     } else if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
@@ -1852,7 +2132,8 @@ wgrt_status wgrt_trace_opts(const wgrt_scene *s, const wgrt_rays *rays, int64_t 
     if (!opts) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL opts");
     if (opts->kernel != 0 && opts->kernel != 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
     return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
-                        opts->variant, opts->workgroups, opts->kernel == 1, opts->chunk_order, opts->n_chunk_order);
+                        opts->variant, opts->workgroups, opts->kernel == 1, opts->chunk_order, opts->n_chunk_order,
+                        opts->num_iter);
 }
 
 wgrt_status wgrt_trace_single_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,

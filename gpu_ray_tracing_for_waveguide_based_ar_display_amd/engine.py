@@ -50,7 +50,7 @@ def rays_to_device(rays: dict, device="cuda") -> dict:
 def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                     gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                     per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                    workgroups: int = 0, chunk_order: torch.Tensor | None = None) -> None:
+                    workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1) -> None:
     """Asynchronous launch on ``stream`` (default: torch's current stream).
 
     rays: dict of device float32 tensors keyed like the reference columns
@@ -59,17 +59,20 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
     accepted too.  stats: optional int64[4] device tensor that is added to
     (bounces, bad_rays, eyebox_hits, replayed).  chunk_order: optional int32 device
     permutation of the 64-ray chunks (``schedule_by_lifetime``); results do not depend on it.
+    num_iter: chained traces of every ray (the reference's ``num_iter`` loop of launches,
+    MAIN:169-177) in one call -- results identical to ``num_iter`` calls; the Jones-vector
+    variants run them in one persistent launch (``wgrt_launch_opts.num_iter``).
     """
     if scene.single_lambda:
         raise ValueError("trace_fullcolor needs a full-colour scene; use trace_single for a single-wavelength one")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=False, chunk_order=chunk_order)
+           workgroups, single=False, chunk_order=chunk_order, num_iter=num_iter)
 
 
 def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                  gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                  per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                 workgroups: int = 0, chunk_order: torch.Tensor | None = None) -> None:
+                 workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1) -> None:
     """One launch of the single-wavelength kernel (``process_rays_kernel_pro``, GRTF:419-831)
     through ``wgrt_trace_single_ex``: no ``lmd_num`` column (ignored if present),
     matrix_EB [NY, NX, 80, 120], branch guard ener * efficiency > 1e-15.  The scene must be
@@ -77,11 +80,11 @@ def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: 
     if not scene.single_lambda:
         raise ValueError("trace_single needs a single-wavelength scene (Scene.from_geometry(..., wavelength=l))")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=True, chunk_order=chunk_order)
+           workgroups, single=True, chunk_order=chunk_order, num_iter=num_iter)
 
 
 def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single, chunk_order=None):
+           workgroups, single, chunk_order=None, num_iter=1):
     device = torch.device("cuda", scene.device)
     x = rays["x"]
     N = x.numel() if n_rays is None else int(n_rays)
@@ -114,7 +117,7 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
         _as_dev(chunk_order, torch.int32, "chunk_order", device, n_chunks)
     opts = LaunchOpts(1 if single else 0, int(variant), int(workgroups),
                       ctypes.c_void_p(chunk_order.data_ptr()) if chunk_order is not None else None,
-                      n_chunks if chunk_order is not None else 0)
+                      n_chunks if chunk_order is not None else 0, int(num_iter))
     check(load().wgrt_trace_opts(
         scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
         ctypes.c_void_p(matrix_EB.data_ptr()),

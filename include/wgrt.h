@@ -172,6 +172,15 @@ typedef struct {
      * engine.schedule_by_lifetime).  The permutation is not validated on the device. */
     const int32_t *chunk_order;
     int64_t n_chunk_order;
+    /* Chained traces per call (0 or 1: one).  num_iter = K gives exactly the results of K
+     * successive launches over the same rays (the reference's num_iter loop, MAIN:169-177):
+     * every ray is traced K times, each trace starting from the RNG state the previous one
+     * left, all out-couplings binned into matrix_EB, rng_states left at the last trace's
+     * states, stats summed over the K traces.  Variants 7-9 run the K traces in ONE
+     * persistent launch (one iteration's straggler tail overlaps the next one's bulk);
+     * the others issue K launches.  1 <= num_iter <= 255; num_iter > 1 needs
+     * per_ray_bounces == NULL and chunk_order == NULL. */
+    int num_iter;
 } wgrt_launch_opts;
 
 /* One launch of either bounce kernel with launch options (everything else as
@@ -197,7 +206,9 @@ wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t n
 
 /* Polygon membership of n points (DEVICE xy[n, 2]) through the scene's locator:
  * bit k of out_mask[i] = is_inside_or_on_edge(point i, polygon k) with polygon order
- * 0 eff_reg1, 1 eff_reg2, 2 IC, 3.. FC slices, then OC slices (GRTF:63-71).  Test hook. */
+ * 0 eff_reg1, 1 eff_reg2, 2 IC, 3.. FC slices, then OC slices (GRTF:63-71).  Bit 63 is set
+ * if the two exact fallbacks the kernels use (CSR row lists, 128-B band records) disagreed
+ * for any polygon.  Test hook. */
 wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64_t n,
                                 uint64_t *out_mask, void *stream);
 

@@ -1,8 +1,11 @@
 #!/bin/bash
+# scratch experiment driver (one gpurun call)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-mkdir -p gpurun_out
-timeout -k 10 400 python -u -m pytest tests/test_gpu_parity.py -m gpu -q -x --timeout 300 --timeout-method thread -k "7 or 8 or 9 or forced or rare or invariance or edge" > gpurun_out/pytest_exp.log 2>&1
-rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/pytest_exp.log
-if [ $rc -ne 0 ] && [ $rc -ne 1 ]; then exit $rc; fi
-timeout -k 10 200 python tools/ab.py --variants 5,7 --rounds 8 > gpurun_out/ab.log 2>&1 || exit $?
-timeout -k 10 200 python tools/phases.py 7 > gpurun_out/phases7.log 2>&1 || exit $?
+OUT=gpurun_out/exp; mkdir -p $OUT
+set -e
+timeout -k 10 200 python tools/ab.py --variants 7f,7f,7f,7f,7f --workgroups 768,640,512,384,1024 --num-iter 4 --rounds 6 > $OUT/wg4.log 2>&1
+timeout -k 10 200 python tools/ab.py --variants 7,7,7,7 --workgroups 768,640,512,384 --num-iter 1 --rounds 6 > $OUT/wg1.log 2>&1
+WGRT_JMAX_HOPS=2 timeout -k 10 200 python tools/ab.py --variants 7f,7 --num-iter 4 --rounds 6 > $OUT/hops2.log 2>&1
+WGRT_JMAX_HOPS=4 timeout -k 10 200 python tools/ab.py --variants 7f,7 --num-iter 4 --rounds 6 > $OUT/hops4.log 2>&1
+timeout -k 10 200 python tools/ab.py --variants 7f,7 --num-iter 16 --rounds 4 > $OUT/it16.log 2>&1
+timeout -k 10 200 python tools/ab.py --variants 7f,7 --num-iter 4 --rounds 4 --R 4096 > $OUT/r4096.log 2>&1

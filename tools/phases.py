@@ -43,7 +43,7 @@ for it in range(4):
     rng = seeds.clone()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    trace_fullcolor(sc, rays, rng, eb, variant=variant)
+    trace_fullcolor(sc, rays, rng, eb, variant=variant, workgroups=int(os.environ.get("PHASE_WG", "0")))
     b.record()
     torch.cuda.synchronize()
     L.wgrt_diag_read_phases(ph, wt)
