@@ -134,10 +134,11 @@ struct TraceArgs {
     int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
     const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
     int jtile_d;
-    // Jones-vector variants: out-couplings, by ray (eb_tag[i] == epoch marks ray i's this launch)
-    double2 *eb_xy;
-    uint32_t *eb_tag;
-    uint32_t epoch;
+    // Jones-vector variants: out-couplings appended as (position, ray index) and binned into
+    // matrix_EB by eyebox_kernel after the launch
+    double2 *q_xy;
+    uint32_t *q_i;
+    unsigned long long *q_count;
     double cert_tol;   // Jones-vector variants: base of the decision certification bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
@@ -742,11 +743,10 @@ struct JLane {
     uint32_t bounces;
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
-    bool hit;                // fused launches: accumulated into matrix_EB
     uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
 
-enum : int { kUncertain = -3 };
+enum : int { kUncertain = -3, kOut = -4 };
 
 __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L) {
 #ifdef WGRT_ABL_RAYLOAD
@@ -781,7 +781,6 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.s = A.rng[ld];
     L.r.region = 0;
     L.bounces = 1;
-    L.hit = false;
     L.pf = 0ull;
     return true;
 }
@@ -842,7 +841,7 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
 // Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
 // kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
 // of it has been written) and replayed.
-template <bool FUSED = false, class Loc>
+template <class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
                                         bool entry) {
     JRay &r = L.r;
@@ -924,15 +923,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 
     if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
         DIAG_REGION(2);
-        if (FUSED) {   // several traces of a ray per launch: bin now
-            const int64_t g = (int64_t)((double)(T - A.jtiles) / (double)A.jtile_d);   // exact: < 2^40
-            const int n = (int)(g % A.ny), m = (int)((g / A.ny) % A.nx), l = (int)(g / ((int64_t)A.ny * A.nx));
-            L.hit = eyebox_add(A, l, m, n, r.x, r.y);
-        } else {       // recorded; eyebox_kernel bins it after the launch
-            A.eb_xy[L.i] = double2{r.x, r.y};
-            A.eb_tag[L.i] = A.epoch;
-        }
-        return kDie;
+        return kOut;   // appended to the out-coupling queue by the caller (at (r.x, r.y))
     }
     DIAG_REGION(1);
     ASM_MARK("interact-take");
@@ -1083,20 +1074,21 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     add_stats(A.stats, b, h, bad);
 }
 
-// Runs right behind every Jones-vector launch on its stream: bins the recorded out-couplings
-// (ray i out-coupled this launch iff eb_tag[i] == epoch) into matrix_EB.
+// Runs right behind every Jones-vector launch on its stream: bins the queued out-couplings
+// (entry j: position q_xy[j] of ray q_i[j]) into matrix_EB -- the eyebox predicate, its
+// divisions and the atomics stay out of the bounce loop.  matrix_EB cells count hits (+1.0f),
+// so the binning order does not matter.
 __global__ __launch_bounds__(256) void eyebox_kernel(TraceArgs A) {
     uint64_t h = 0;
-    for (int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x; i < A.n_rays;
-         i += (int64_t)gridDim.x * blockDim.x) {
-        if (A.eb_tag[i] != A.epoch) continue;
-#ifdef WGRT_ABL_EBSCAN
-        h += 1;   // ablation build only: scan the tags, bin nothing
-#else
-        const double2 p = A.eb_xy[i];
+    const unsigned long long nq = *A.q_count;
+    for (unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq;
+         j += (unsigned long long)gridDim.x * blockDim.x) {
+        const uint32_t qi = A.q_i[j];
+        if (qi == 0xffffffffu) continue;   // a slot its wave left unused
+        const int64_t i = qi;
+        const double2 p = A.q_xy[j];
         const int m = (int)A.m[i], n = (int)A.n[i], l = A.l ? (int)A.l[i] : 0;
         h += eyebox_add(A, l, m, n, p.x, p.y);
-#endif
     }
     add_stats(A.stats, 0, h, 0);
 }
@@ -1141,7 +1133,8 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
 // XCD id steers placement only: any wave may take any chunk, so correctness never depends on it.
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
-constexpr int kScratchCtr = (kHeads + 1) * kHeadStride;   // heads + replay count
+constexpr int kScratchCtr = (kHeads + 2) * kHeadStride;   // heads, replay count, out-coupling slots
+constexpr int kQBlock = 512;   // out-coupling queue slots a wave reserves at a time
 
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
@@ -1418,7 +1411,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
-    uint32_t tot_b = 0, tot_h = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
+    uint32_t tot_b = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
+    unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
+    int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
 
     // head x's items: iteration-major over its chunk range [lo, hi)
     auto decode = [&](int x, int64_t q, int64_t &c, uint32_t &k) -> bool {
@@ -1458,7 +1453,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     };
     auto retire = [&]() {
         tot_b += L.bounces;
-        tot_h += L.hit;
         if (FUSED && (int64_t)L.k + 1 < n_iter) {
             __hip_atomic_store(A.rng64 + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -1526,9 +1520,13 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             need = __ballot(!active && !waiting);
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
+        bool out = false;
         if (active && blk >= 0) {
-            const int next = interact<FUSED>(A, loc, L, blk, kind, entry);
-            if (next == kUncertain) {
+            const int next = interact(A, loc, L, blk, kind, entry);
+            if (next == kOut) {
+                out = true;
+                retire();
+            } else if (next == kUncertain) {
                 // abandoned with no side effect; replay_kernel re-traces it (fused: from this
                 // iteration on, so later iterations skip the ray)
                 if (FUSED)
@@ -1542,8 +1540,32 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 L.r.region = next;
             }
         }
+        // out-couplings of this pass go to the wave's block of queue slots (a contended returning
+        // atomic per pass would put its latency on every pass; a new block is needed about
+        // once per hundred passes)
+        const uint64_t om = __ballot(out);
+        if (om != 0ull) {
+            const int nout = __popcll(om), rank = __popcll(om & lt_mask), rem = kQBlock - qfill;
+            unsigned long long nb = 0;
+            if (nout > rem) {
+                if (lane == 0) nb = atomicAdd(A.q_count, (unsigned long long)kQBlock);
+                nb = __shfl(nb, 0);
+            }
+            if (out) {
+                const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
+                A.q_xy[j] = double2{L.r.x, L.r.y};
+                A.q_i[j] = (uint32_t)L.i;
+            }
+            if (nout > rem) {
+                qbase = nb;
+                qfill = nout - rem;
+            } else {
+                qfill += nout;
+            }
+        }
     }
-    add_stats(A.stats, tot_b, tot_h, tot_bad);
+    for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
+    add_stats(A.stats, tot_b, 0, tot_bad);
 }
 
 // Variants 7-9: the persistent loop over the Jones-vector path (32-bit cell words at W waves
@@ -1693,10 +1715,10 @@ struct wgrt_scene {
     struct Scratch {
         unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), then the replay count
         uint32_t *list = nullptr;            // replay list
-        double2 *eb_xy = nullptr;            // out-couplings by ray: position, launch tag
-        uint32_t *eb_tag = nullptr;
-        uint32_t epoch = 0;
-        int64_t cap = 0;
+        int64_t cap = 0;                     // replay list entries
+        double2 *q_xy = nullptr;             // out-coupling queue: position, ray index
+        uint32_t *q_i = nullptr;
+        int64_t qcap = 0;
         uint64_t *rng64 = nullptr;           // fused launches: per-ray {state, tag} granules
         uint32_t iter_epoch = 0;             // < 2^23 (iter_tag)
         int64_t cap64 = 0;
@@ -1849,8 +1871,8 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     for (auto &kv : s->scratch) {
         (void)hipFree(kv.second.ctr);
         (void)hipFree(kv.second.list);
-        (void)hipFree(kv.second.eb_xy);
-        (void)hipFree(kv.second.eb_tag);
+        (void)hipFree(kv.second.q_xy);
+        (void)hipFree(kv.second.q_i);
         (void)hipFree(kv.second.rng64);
     }
     delete s;
@@ -1949,14 +1971,18 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.replay_list = nullptr;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
-    A.eb_xy = nullptr;
-    A.eb_tag = nullptr;
-    A.epoch = 0;
+    A.q_xy = nullptr;
+    A.q_i = nullptr;
+    A.q_count = nullptr;
     A.n_iter = 1;
     A.rng64 = nullptr;
     A.iter_epoch = 0;
     hipStream_t st = (hipStream_t)stream;
     if (variant >= 7) {
+        int64_t grid = workgroups > 0 ? workgroups
+                                      : (variant == 7 ? s->jones_grid : variant == 8 ? s->jones_w4_grid : s->jones64_grid);
+        const int64_t useful = (n_rays + 255) / 256;
+        if (grid > useful) grid = useful;
         wgrt_scene *ms = const_cast<wgrt_scene *>(s);
         wgrt_scene::Scratch *sc;
         {
@@ -1970,19 +1996,27 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
                 // the old lists may still be in use by this stream's previous launch
                 HIP_TRY(hipStreamSynchronize(st));
                 (void)hipFree(sc->list);
-                (void)hipFree(sc->eb_xy);
-                (void)hipFree(sc->eb_tag);
-                sc->list = sc->eb_tag = nullptr;
-                sc->eb_xy = nullptr;
+                sc->list = nullptr;
                 sc->cap = 0;
-                sc->epoch = 0;
                 hipError_t e = hipMalloc((void **)&sc->list, (size_t)n_rays * sizeof(uint32_t));
-                if (e == hipSuccess) e = hipMalloc((void **)&sc->eb_xy, (size_t)n_rays * sizeof(double2));
-                if (e == hipSuccess) e = hipMalloc((void **)&sc->eb_tag, (size_t)n_rays * sizeof(uint32_t));
-                if (e == hipSuccess) e = hipMemset(sc->eb_tag, 0, (size_t)n_rays * sizeof(uint32_t));
                 if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
                 if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
                 sc->cap = n_rays;
+            }
+            // a trace out-couples at most once; each wave leaves at most one block partly unused
+            const int64_t qn = n_rays * num_iter + grid * 4 * kQBlock;
+            if (sc->qcap < qn) {
+                HIP_TRY(hipStreamSynchronize(st));
+                (void)hipFree(sc->q_xy);
+                (void)hipFree(sc->q_i);
+                sc->q_xy = nullptr;
+                sc->q_i = nullptr;
+                sc->qcap = 0;
+                hipError_t e = hipMalloc((void **)&sc->q_xy, (size_t)qn * sizeof(double2));
+                if (e == hipSuccess) e = hipMalloc((void **)&sc->q_i, (size_t)qn * sizeof(uint32_t));
+                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+                sc->qcap = qn;
             }
             if (num_iter > 1 && sc->cap64 < n_rays) {
                 HIP_TRY(hipStreamSynchronize(st));
@@ -2008,20 +2042,12 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         }
         A.replay_count = sc->ctr + kHeads * kHeadStride;
         A.replay_list = sc->list;
-        if (++sc->epoch == 0) {   // tags wrapped (after 2^32 launches): clear them
-            HIP_TRY(hipMemsetAsync(sc->eb_tag, 0, (size_t)sc->cap * sizeof(uint32_t), st));
-            sc->epoch = 1;
-        }
-        A.eb_xy = sc->eb_xy;
-        A.eb_tag = sc->eb_tag;
-        A.epoch = sc->epoch;
+        A.q_xy = sc->q_xy;
+        A.q_i = sc->q_i;
+        A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
         HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
         const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
         A.max_hops = g_jmax_hops;
-        int64_t grid = workgroups > 0 ? workgroups
-                                      : (variant == 7 ? s->jones_grid : variant == 8 ? s->jones_w4_grid : s->jones64_grid);
-        const int64_t useful = (n_rays + 255) / 256;
-        if (grid > useful) grid = useful;
         LocatorT<uint32_t> l32;
         l32.cells = s->d_cells32;
         l32.verts = A.loc.verts;
@@ -2047,11 +2073,8 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
             hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, A.loc,
                                sc->ctr, jchunk);
         HIP_TRY(hipGetLastError());
-        if (num_iter == 1) {   // fused launches bin their out-couplings inline
-            const int64_t eblocks = std::min<int64_t>((n_rays + 255) / 256, 2048);
-            hipLaunchKernelGGL(eyebox_kernel, dim3((unsigned)eblocks), dim3(256), 0, st, A);
-            HIP_TRY(hipGetLastError());
-        }
+        hipLaunchKernelGGL(eyebox_kernel, dim3(1024), dim3(256), 0, st, A);
+        HIP_TRY(hipGetLastError());
         hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
     } else if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
