@@ -16,7 +16,7 @@ LIB_PATH = os.path.join(PKG, "libwgrt.so")
 
 ABI_VERSION = 1
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
-            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
+            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -117,6 +117,8 @@ def load(path: str = LIB_PATH):
                                              ctypes.c_int64, _vp]
     L.wgrt_selftest_math.restype = st
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
+    L.wgrt_scene_reserve.restype = st
+    L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
     L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
     L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
     L.wgrt_status_string.restype = ctypes.c_char_p

@@ -1894,6 +1894,60 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     return WGRT_OK;
 }
 
+// The Jones-vector variants' per-stream launch scratch (work-queue heads, replay list,
+// out-coupling queue, fused-launch granules), grown to n_rays x num_iter traces on `grid`
+// workgroups.  Growing synchronises the stream (the old buffers may be in use).
+static wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num_iter, int64_t grid,
+                                  wgrt_scene::Scratch **out) {
+    hipStream_t st = (hipStream_t)stream;
+    std::lock_guard<std::mutex> lk(ms->scratch_mu);
+    wgrt_scene::Scratch *sc = &ms->scratch[stream];
+    *out = sc;
+    if (!sc->ctr) {
+        hipError_t e = hipMalloc((void **)&sc->ctr, kScratchCtr * sizeof(unsigned long long));
+        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+    }
+    if (sc->cap < n_rays) {
+        // the old lists may still be in use by this stream's previous launch
+        HIP_TRY(hipStreamSynchronize(st));
+        (void)hipFree(sc->list);
+        sc->list = nullptr;
+        sc->cap = 0;
+        hipError_t e = hipMalloc((void **)&sc->list, (size_t)n_rays * sizeof(uint32_t));
+        if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+        sc->cap = n_rays;
+    }
+    // a trace out-couples at most once; each wave leaves at most one block partly unused
+    const int64_t qn = n_rays * num_iter + grid * 4 * kQBlock;
+    if (sc->qcap < qn) {
+        HIP_TRY(hipStreamSynchronize(st));
+        (void)hipFree(sc->q_xy);
+        (void)hipFree(sc->q_i);
+        sc->q_xy = nullptr;
+        sc->q_i = nullptr;
+        sc->qcap = 0;
+        hipError_t e = hipMalloc((void **)&sc->q_xy, (size_t)qn * sizeof(double2));
+        if (e == hipSuccess) e = hipMalloc((void **)&sc->q_i, (size_t)qn * sizeof(uint32_t));
+        if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+        sc->qcap = qn;
+    }
+    if (num_iter > 1 && sc->cap64 < n_rays) {
+        HIP_TRY(hipStreamSynchronize(st));
+        (void)hipFree(sc->rng64);
+        sc->rng64 = nullptr;
+        sc->cap64 = 0;
+        sc->iter_epoch = 0;
+        hipError_t e = hipMalloc((void **)&sc->rng64, (size_t)n_rays * sizeof(uint64_t));
+        if (e == hipSuccess) e = hipMemset(sc->rng64, 0, (size_t)n_rays * sizeof(uint64_t));
+        if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
+        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+        sc->cap64 = n_rays;
+    }
+    return WGRT_OK;
+}
+
 // One launch of the bounce kernel.  single: the single-wavelength kernel
 // process_rays_kernel_pro (GRTF:419-831) -- no lmd_num column, wavelength 0 of a
 // one-wavelength scene, threshold 1e-15; otherwise process_rays_kernel_pro_fullColor
@@ -1984,52 +2038,10 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         const int64_t useful = (n_rays + 255) / 256;
         if (grid > useful) grid = useful;
         wgrt_scene *ms = const_cast<wgrt_scene *>(s);
-        wgrt_scene::Scratch *sc;
+        wgrt_scene::Scratch *sc = nullptr;
         {
-            std::lock_guard<std::mutex> lk(ms->scratch_mu);
-            sc = &ms->scratch[stream];
-            if (!sc->ctr) {
-                hipError_t e = hipMalloc((void **)&sc->ctr, kScratchCtr * sizeof(unsigned long long));
-                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
-            }
-            if (sc->cap < n_rays) {
-                // the old lists may still be in use by this stream's previous launch
-                HIP_TRY(hipStreamSynchronize(st));
-                (void)hipFree(sc->list);
-                sc->list = nullptr;
-                sc->cap = 0;
-                hipError_t e = hipMalloc((void **)&sc->list, (size_t)n_rays * sizeof(uint32_t));
-                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
-                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
-                sc->cap = n_rays;
-            }
-            // a trace out-couples at most once; each wave leaves at most one block partly unused
-            const int64_t qn = n_rays * num_iter + grid * 4 * kQBlock;
-            if (sc->qcap < qn) {
-                HIP_TRY(hipStreamSynchronize(st));
-                (void)hipFree(sc->q_xy);
-                (void)hipFree(sc->q_i);
-                sc->q_xy = nullptr;
-                sc->q_i = nullptr;
-                sc->qcap = 0;
-                hipError_t e = hipMalloc((void **)&sc->q_xy, (size_t)qn * sizeof(double2));
-                if (e == hipSuccess) e = hipMalloc((void **)&sc->q_i, (size_t)qn * sizeof(uint32_t));
-                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
-                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
-                sc->qcap = qn;
-            }
-            if (num_iter > 1 && sc->cap64 < n_rays) {
-                HIP_TRY(hipStreamSynchronize(st));
-                (void)hipFree(sc->rng64);
-                sc->rng64 = nullptr;
-                sc->cap64 = 0;
-                sc->iter_epoch = 0;
-                hipError_t e = hipMalloc((void **)&sc->rng64, (size_t)n_rays * sizeof(uint64_t));
-                if (e == hipSuccess) e = hipMemset(sc->rng64, 0, (size_t)n_rays * sizeof(uint64_t));
-                if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
-                if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
-                sc->cap64 = n_rays;
-            }
+            const wgrt_status e = ensure_scratch(ms, stream, n_rays, num_iter, grid, &sc);
+            if (e != WGRT_OK) return e;
         }
         if (num_iter > 1) {
             if (++sc->iter_epoch >= (1u << 23)) {   // granule tags wrapped: clear them
@@ -2132,6 +2144,16 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     }
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
+}
+
+wgrt_status wgrt_scene_reserve(const wgrt_scene *s, int64_t n_rays, int num_iter, void *stream) {
+    if (!s) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene");
+    if (n_rays < 0 || num_iter < 0 || num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "bad n_rays / num_iter");
+    if (n_rays == 0) return WGRT_OK;
+    const int64_t grid = std::max<int64_t>(std::max<int64_t>(s->jones_grid, s->jones_w4_grid), s->jones64_grid);
+    wgrt_scene::Scratch *sc = nullptr;
+    return ensure_scratch(const_cast<wgrt_scene *>(s), stream, n_rays, std::max(num_iter, 1),
+                          std::min<int64_t>(grid, (n_rays + 255) / 256), &sc);
 }
 
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays,

@@ -69,6 +69,15 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
            workgroups, single=False, chunk_order=chunk_order, num_iter=num_iter)
 
 
+def reserve(scene: Scene, n_rays: int, num_iter: int = 1, stream=None) -> None:
+    """Pre-allocate the Jones-vector variants' launch scratch for up to ``n_rays`` rays x
+    ``num_iter`` chained traces on ``stream`` (``wgrt_scene_reserve``): later launches within
+    those sizes neither allocate nor synchronise."""
+    device = torch.device("cuda", scene.device)
+    check(load().wgrt_scene_reserve(scene.handle, int(n_rays), int(num_iter),
+                                    ctypes.c_void_p(_stream_handle(device, stream))), "wgrt_scene_reserve")
+
+
 def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                  gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                  per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,

@@ -189,6 +189,13 @@ wgrt_status wgrt_trace_opts(const wgrt_scene *scene, const wgrt_rays *rays, int6
                             uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
                             uint32_t *per_ray_bounces, void *stream, const wgrt_launch_opts *opts);
 
+/* Pre-allocates the launch scratch the Jones-vector variants (7-9) use on `stream` for
+ * launches of up to n_rays rays x num_iter chained traces (work-queue heads, replay list,
+ * out-coupling queue, fused-launch hand-off words), so that no later launch within those
+ * sizes allocates or synchronises.  Optional: a launch grows the scratch itself.  Not part
+ * of the reference (its launches allocate nothing on the device). */
+wgrt_status wgrt_scene_reserve(const wgrt_scene *scene, int64_t n_rays, int num_iter, void *stream);
+
 /* Device-side ray setup (replaces the host loop MAIN:59-115 and the seeding at MAIN:158):
  * fills FoV x wavelength blocks [block_lo, block_hi) of the batch -- block b =
  * (ii * ny + jj) * n_lambdas + k, rays [b * R, (b + 1) * R) -- into DEVICE columns of
