@@ -1414,6 +1414,16 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     uint32_t tot_b = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
+#ifdef WGRT_PHASES
+    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
+    const int p_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGRT_DIAG
+    uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_wait = 0;
+    const int d_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid] = __builtin_amdgcn_s_memrealtime();
+#endif
 
     // head x's items: iteration-major over its chunk range [lo, hi)
     auto decode = [&](int x, int64_t q, int64_t &c, uint32_t &k) -> bool {
@@ -1464,11 +1474,18 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     };
 
     for (;;) {
+#ifdef WGRT_PHASES
+        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
+        const int pofs = exhausted ? 4 : 0;
+#endif
         if (active) {
             blk = advance(A, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
+#ifdef WGRT_PHASES
+        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
+#endif
         if (FUSED && waiting) start();   // poll the previous trace's granule again
         uint64_t need = __ballot(!active && !waiting);
         while (need != 0ull && !exhausted) {
@@ -1496,6 +1513,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 pend_h = -1;
                 if (!got) {
                     exhausted = true;
+#ifdef WGRT_PHASES
+                    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
+#ifdef WGRT_DIAG
+                    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 1] = __builtin_amdgcn_s_memrealtime();
+#endif
                     break;
                 }
                 pend_h = head;   // issue the next dequeue now; read when this item runs dry
@@ -1521,6 +1544,22 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
         bool out = false;
+#ifdef WGRT_PHASES
+        const uint64_t pt2 = __builtin_amdgcn_s_memtime();
+#endif
+#ifdef WGRT_DIAG
+        {
+            const uint64_t na = __popcll(__ballot(active && blk >= 0));
+            d_pass += 1;
+            d_act += na;
+            d_wait += __popcll(__ballot(waiting));
+            if (exhausted) {
+                d_pass_x += 1;
+                d_act_x += na;
+            }
+            d_hops += (active && blk == kTransit) ? 1 : 0;
+        }
+#endif
         if (active && blk >= 0) {
             const int next = interact(A, loc, L, blk, kind, entry);
             if (next == kOut) {
@@ -1563,9 +1602,36 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 qfill += nout;
             }
         }
+#ifdef WGRT_PHASES
+        {
+            const uint64_t pt3 = __builtin_amdgcn_s_memtime();
+            ph[pofs + 0] += pt1 - pt0;
+            ph[pofs + 1] += pt2 - pt1;
+            ph[pofs + 2] += pt3 - pt2;
+            ph[pofs + 3] += 1;
+        }
+#endif
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
     add_stats(A.stats, tot_b, 0, tot_bad);
+#ifdef WGRT_PHASES
+    if (lane == 0) {
+        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
+        if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
+    }
+#endif
+#ifdef WGRT_DIAG
+    if (lane == 0) {
+        if (d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 2] = __builtin_amdgcn_s_memrealtime();
+        atomicAdd(&g_diag[0], d_pass);
+        atomicAdd(&g_diag[1], d_act);
+        atomicAdd(&g_diag[2], d_pass_x);
+        atomicAdd(&g_diag[3], d_act_x);
+        atomicAdd(&g_diag[5], d_wait);
+    }
+    d_hops = wave_sum(d_hops);
+    if (lane == 0) atomicAdd(&g_diag[4], d_hops);
+#endif
 }
 
 // Variants 7-9: the persistent loop over the Jones-vector path (32-bit cell words at W waves

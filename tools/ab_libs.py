@@ -30,7 +30,7 @@ ts = []; bs = []; rs = None
 for k in range(15):
     rng = seeds.clone(); st = torch.zeros(4, dtype=torch.int64, device=dev)
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    a.record(); trace_fullcolor(sc, rays, rng, eb, n_rays=n, stats=st, variant=%(variant)d); b.record()
+    a.record(); trace_fullcolor(sc, rays, rng, eb, n_rays=n, stats=st, variant=%(variant)d, num_iter=%(k)d); b.record()
     torch.cuda.synchronize()
     if k >= 3: ts.append(a.elapsed_time(b)); bs.append(int(st[0]))
     if rs is None: rs = int(rng[:n].double().sum().item())
@@ -43,13 +43,14 @@ def main():
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--n", type=int, default=0)
+    ap.add_argument("--num-iter", type=int, default=1)
     ap.add_argument("libs", nargs="+")
     a = ap.parse_args()
     res = {lib: [] for lib in a.libs}
     for _ in range(a.rounds):
         for lib in a.libs:
             r = subprocess.run([sys.executable, "-c", RUN % dict(repo=REPO, lib=os.path.abspath(lib), n=a.n,
-                                                                  variant=a.variant)],
+                                                                  variant=a.variant, k=a.num_iter)],
                                capture_output=True, text=True, timeout=300)
             line = [l for l in r.stdout.splitlines() if l.startswith("{")]
             if not line:

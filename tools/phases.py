@@ -43,13 +43,14 @@ for it in range(4):
     rng = seeds.clone()
     a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     a.record()
-    trace_fullcolor(sc, rays, rng, eb, variant=variant, workgroups=int(os.environ.get("PHASE_WG", "0")))
+    trace_fullcolor(sc, rays, rng, eb, variant=variant, workgroups=int(os.environ.get("PHASE_WG", "0")),
+                    num_iter=int(os.environ.get("PHASE_ITER", "1")))
     b.record()
     torch.cuda.synchronize()
     L.wgrt_diag_read_phases(ph, wt)
 ms = a.elapsed_time(b)
 p = list(ph)
-print(f"variant={variant} R={R} kernel {ms:.3f} ms")
+print(f"variant={variant} R={R} num_iter={os.environ.get('PHASE_ITER', '1')} flags={extra} kernel {ms:.3f} ms")
 for tag, o in (("before dry", 0), ("after dry ", 4)):
     n = max(p[o + 3], 1)
     tot = p[o] + p[o + 1] + p[o + 2]
