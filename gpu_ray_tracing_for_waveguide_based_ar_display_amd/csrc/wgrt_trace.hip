@@ -149,6 +149,21 @@ struct TraceArgs {
     uint32_t iter_epoch;
 };
 
+// A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
+// used (a volatile scalar load, a scalar-cache hit) instead of being held in an SGPR for the
+// whole kernel: the Jones loop keeps only its per-pass operands in SGPRs; the ray columns and
+// the rare-path pointers (refill, retire, replay, out-coupling) are fetched when those run.
+// Valid only in kernels whose first parameter is the TraceArgs.
+template <class T>
+__device__ __forceinline__ T karg(size_t off) {
+    typedef volatile const T __attribute__((address_space(4))) *VP;
+    const char __attribute__((address_space(4))) *base =
+        (const char __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(VP)(base + off);
+}
+#define KA(f) karg<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
+
+
 constexpr int kPolyEff1 = 0;
 constexpr int kPolyEff2 = 1;
 constexpr int kPolyIC = 2;
@@ -754,18 +769,19 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
 #else
     const int64_t ld = i;
 #endif
-    const int m = (int)A.m[ld], n = (int)A.n[ld], l = A.l ? (int)A.l[ld] : 0;
+    const float *const cl = KA(l);
+    const int m = (int)KA(m)[ld], n = (int)KA(n)[ld], l = cl ? (int)cl[ld] : 0;
     if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
     L.i = i;
 #ifdef WGRT_ABL_TILE
     L.T = A.jtiles;   // ablation build only: every ray reads tile 0
 #else
-    L.T = A.jtiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d;
+    L.T = KA(jtiles) + (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d;
 #endif
-    L.r.x = (double)A.x[ld];
-    L.r.y = (double)A.y[ld];
-    const double te = (double)A.te[ld], tm = (double)A.tm[ld];
-    const float d = A.dph[ld];
+    L.r.x = (double)KA(x)[ld];
+    L.r.y = (double)KA(y)[ld];
+    const double te = (double)KA(te)[ld], tm = (double)KA(tm)[ld];
+    const float d = KA(dph)[ld];
     double sd = 0.0, cd = 1.0;
     if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
     // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
@@ -778,7 +794,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.eerr = 0.0;
     L.r.gx = L.r.gy = 0.0;
     L.r.hops = 0;
-    L.r.s = A.rng[ld];
+    L.r.s = KA(rng)[ld];
     L.r.region = 0;
     L.bounces = 1;
     L.pf = 0ull;
@@ -964,6 +980,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     JRay &r = L.r;
+    ASM_MARK("advance");
     for (int hops = 0;; ++hops) {
         if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
         DIAG_REGION(3);
@@ -1444,7 +1461,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             return;
         }
         if (FUSED && L.k > 0) {
-            const uint64_t w = __hip_atomic_load(A.rng64 + L.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t w = __hip_atomic_load(KA(rng64) + L.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t tag = (uint32_t)w;
             if (tag == iter_tag(A.iter_epoch, L.k, false)) {
                 L.r.s = (uint32_t)(w >> 32);
@@ -1464,11 +1481,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     auto retire = [&]() {
         tot_b += L.bounces;
         if (FUSED && (int64_t)L.k + 1 < n_iter) {
-            __hip_atomic_store(A.rng64 + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
+            __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         } else {
-            A.rng[L.i] = L.r.s;
-            if (!FUSED && A.per_ray) A.per_ray[L.i] = L.bounces;
+            KA(rng)[L.i] = L.r.s;
+            uint32_t *const pr = KA(per_ray);
+            if (!FUSED && pr) pr[L.i] = L.bounces;
         }
         active = false;
     };
@@ -1478,6 +1496,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         const uint64_t pt0 = __builtin_amdgcn_s_memtime();
         const int pofs = exhausted ? 4 : 0;
 #endif
+        ASM_MARK("pass-top");
         if (active) {
             blk = advance(A, loc, L, kind);
             entry = false;
@@ -1486,6 +1505,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 #ifdef WGRT_PHASES
         const uint64_t pt1 = __builtin_amdgcn_s_memtime();
 #endif
+        ASM_MARK("refill");
         if (FUSED && waiting) start();   // poll the previous trace's granule again
         uint64_t need = __ballot(!active && !waiting);
         while (need != 0ull && !exhausted) {
@@ -1523,9 +1543,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 }
                 pend_h = head;   // issue the next dequeue now; read when this item runs dry
                 if (lane == 0) pend_v = atomicAdd(heads + kHeadStride * head, 1ull);
-                const int64_t cc = (!FUSED && A.order) ? (int64_t)A.order[c] : c;
+                const int32_t *const ord = KA(order);
+                const int64_t cc = (!FUSED && ord) ? (int64_t)ord[c] : c;
                 cur = cc * chunk;
-                end = cur + chunk < A.n_rays ? cur + chunk : A.n_rays;
+                const int64_t nr = KA(n_rays);
+                end = cur + chunk < nr ? cur + chunk : nr;
                 cur_k = k;
             }
             const int want = __popcll(need);
@@ -1543,6 +1565,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             need = __ballot(!active && !waiting);
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
+        ASM_MARK("pre-interact");
         bool out = false;
 #ifdef WGRT_PHASES
         const uint64_t pt2 = __builtin_amdgcn_s_memtime();
@@ -1569,9 +1592,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 // abandoned with no side effect; replay_kernel re-traces it (fused: from this
                 // iteration on, so later iterations skip the ray)
                 if (FUSED)
-                    __hip_atomic_store(A.rng64 + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
+                    __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                A.replay_list[atomicAdd(A.replay_count, 1ull)] = (uint32_t)L.i;
+                KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
                 active = false;
             } else if (next < 0) {
                 retire();
@@ -1579,6 +1602,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 L.r.region = next;
             }
         }
+        ASM_MARK("post-interact");
         // out-couplings of this pass go to the wave's block of queue slots (a contended returning
         // atomic per pass would put its latency on every pass; a new block is needed about
         // once per hundred passes)
@@ -1587,13 +1611,13 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             const int nout = __popcll(om), rank = __popcll(om & lt_mask), rem = kQBlock - qfill;
             unsigned long long nb = 0;
             if (nout > rem) {
-                if (lane == 0) nb = atomicAdd(A.q_count, (unsigned long long)kQBlock);
+                if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
                 nb = __shfl(nb, 0);
             }
             if (out) {
                 const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
-                A.q_xy[j] = double2{L.r.x, L.r.y};
-                A.q_i[j] = (uint32_t)L.i;
+                KA(q_xy)[j] = double2{L.r.x, L.r.y};
+                KA(q_i)[j] = (uint32_t)L.i;
             }
             if (nout > rem) {
                 qbase = nb;
@@ -1613,7 +1637,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 #endif
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
-    add_stats(A.stats, tot_b, 0, tot_bad);
+    add_stats(KA(stats), tot_b, 0, tot_bad);
 #ifdef WGRT_PHASES
     if (lane == 0) {
         for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
