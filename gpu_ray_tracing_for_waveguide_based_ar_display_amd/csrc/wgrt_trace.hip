@@ -162,6 +162,8 @@ __device__ __forceinline__ T karg(size_t off) {
     return *(VP)(base + off);
 }
 #define KA(f) karg<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
+// the same for the locator's exact-test arrays (TraceArgs::loc holds them for every variant)
+#define KLOC(f) karg<decltype(Locator::f)>(offsetof(TraceArgs, loc) + offsetof(Locator, f))
 
 
 constexpr int kPolyEff1 = 0;
@@ -272,7 +274,7 @@ __device__ __forceinline__ typename Loc::Word locate_w(const Loc &L, double x, d
     return L.cells[(int)fy * L.ncx + (int)fx];
 }
 
-template <class Loc>
+template <bool KARG = false, class Loc>
 __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y) {
     const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
@@ -284,7 +286,8 @@ __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, in
     const int r = k * L.ncy + cy;
     // one 128-B record: the (at most kBandSegs) edges of polygon k meeting this cell row,
     // evaluated with the reference predicate's operations (GRTF:36-71); NaN slots are inert
-    const double4 *rec = (const double4 *)(L.bands + (size_t)r * 4 * kBandSegs);
+    const double *const bands = KARG ? KLOC(bands) : L.bands;
+    const double4 *rec = (const double4 *)(bands + (size_t)r * 4 * kBandSegs);
     const double4 s0 = rec[0], s1 = rec[1], s2 = rec[2], s3 = rec[3];
     if (s0.x != INFINITY) {
         bool inside = false;
@@ -297,12 +300,15 @@ __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, in
         }
         return inside;
     }
-    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
-    const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
-    return inside_or_on_edge_subset(x, y, L.verts + 2 * a, nv, L.row_edges + e0, e1 - e0);
+    const int32_t *const po = KARG ? KLOC(poly_off) : L.poly_off;
+    const int32_t *const ro = KARG ? KLOC(row_off) : L.row_off;
+    const int a = po[k], nv = po[k + 1] - a;
+    const int e0 = ro[r], e1 = ro[r + 1];
+    return inside_or_on_edge_subset(x, y, (KARG ? KLOC(verts) : L.verts) + 2 * a, nv,
+                                    (KARG ? KLOC(row_edges) : L.row_edges) + e0, e1 - e0);
 }
 
-template <class Loc>
+template <bool KARG = false, class Loc>
 __device__ __forceinline__ int first_slice_w(const Loc &L, typename Loc::Word w, int first, int count, double x,
                                              double y) {
     uint64_t f = (uint64_t)w >> (2 * first);
@@ -313,7 +319,7 @@ __device__ __forceinline__ int first_slice_w(const Loc &L, typename Loc::Word w,
         const int p = __builtin_ctzll(cand);
         const int sl = p >> 1;
         if ((in >> p) & 1ull) return sl;
-        if (in_poly_w(L, w, first + sl, x, y)) return sl;
+        if (in_poly_w<KARG>(L, w, first + sl, x, y)) return sl;
         cand &= cand - 1ull;
     }
     return -1;
@@ -763,25 +769,32 @@ struct JLane {
 
 enum : int { kUncertain = -3, kOut = -4 };
 
-__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L) {
+// Every column load is issued before anything branches on a loaded value, so a refill waits
+// for one memory round trip (not one for the FoV / wavelength indices and another for the
+// rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
+                                          uint64_t *gword = nullptr) {
 #ifdef WGRT_ABL_RAYLOAD
     const int64_t ld = (i & 63) | (i & ~(int64_t)1023);   // ablation build only: 64 cache-hot rays per block
 #else
     const int64_t ld = i;
 #endif
     const float *const cl = KA(l);
-    const int m = (int)KA(m)[ld], n = (int)KA(n)[ld], l = cl ? (int)cl[ld] : 0;
-    if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
+    const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
+    const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
+    const uint32_t rs = KA(rng)[ld];
+    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = (int)fm, n = (int)fn, l = (int)fl;
+    const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
     L.i = i;
 #ifdef WGRT_ABL_TILE
     L.T = A.jtiles;   // ablation build only: every ray reads tile 0
 #else
-    L.T = KA(jtiles) + (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d;
+    L.T = KA(jtiles) + (ok ? (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d : 0);
 #endif
-    L.r.x = (double)KA(x)[ld];
-    L.r.y = (double)KA(y)[ld];
-    const double te = (double)KA(te)[ld], tm = (double)KA(tm)[ld];
-    const float d = KA(dph)[ld];
+    L.r.x = (double)fx;
+    L.r.y = (double)fy;
+    const double te = (double)fte, tm = (double)ftm;
     double sd = 0.0, cd = 1.0;
     if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
     // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
@@ -794,11 +807,11 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.eerr = 0.0;
     L.r.gx = L.r.gy = 0.0;
     L.r.hops = 0;
-    L.r.s = KA(rng)[ld];
+    L.r.s = rs;
     L.r.region = 0;
     L.bounces = 1;
     L.pf = 0ull;
-    return true;
+    return ok;
 }
 
 struct JField {
@@ -965,7 +978,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     ASM_MARK("interact-take-end");
     if (kind == 0) {
         DIAG_REGION(5);
-        const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -987,7 +1000,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
         const auto c = (typename Loc::Word)L.pf;
-        if (!in_poly_w(loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        if (!in_poly_w<true>(loc, c, kPolyEff1, r.x, r.y)) return kDie;
         const int region = r.region;
         if (region <= 1) {
             kind = 0;
@@ -996,13 +1009,13 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
         const bool fc = region <= 3;
         const int first = fc ? kPolyFC0 : kPolyFC0 + A.nfc, count = fc ? A.nfc : A.noc;
-        const int s = first_slice_w(loc, c, first, count, r.x, r.y);
+        const int s = first_slice_w<true>(loc, c, first, count, r.x, r.y);
         if (s >= 0) {
             kind = region - 1;
             return (fc ? 3 + (region - 2) * A.nfc : 3 + 2 * A.nfc + (region - 4) * A.noc) + s;
         }
         if (region == 5) return kDie;   // GRTF:1244-1246
-        if (region == 3 && !in_poly_w(loc, c, kPolyEff2, r.x, r.y)) {
+        if (region == 3 && !in_poly_w<true>(loc, c, kPolyEff2, r.x, r.y)) {
             r.region = 4;   // GRTF:1103-1104: no move, same miss hop (gap[2:4], 2 TIR[1])
             continue;
         }
@@ -1453,7 +1466,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     // start the trace (L.i, L.k) on this lane: active, waiting (previous trace still running) or
     // skipped (bad ray / ray already handed to the replay)
     auto start = [&]() {
-        const bool ok = lane_load(A, L.i, L);
+        uint64_t w = 0;
+        const bool ok = lane_load(A, L.i, L, (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
         waiting = false;
         active = false;
         if (!ok) {
@@ -1461,7 +1475,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             return;
         }
         if (FUSED && L.k > 0) {
-            const uint64_t w = __hip_atomic_load(KA(rng64) + L.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
             const uint32_t tag = (uint32_t)w;
             if (tag == iter_tag(A.iter_epoch, L.k, false)) {
                 L.r.s = (uint32_t)(w >> 32);
