@@ -56,7 +56,7 @@ thread_local std::string g_last_error;
 // the smallest power-of-two multiple of twice this size that fits the LDS budget.
 double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
-    return v ? atof(v) : 0.015625;   // 1/64 mm: 37 MB grid at the reference design; fastest on C3
+    return v ? atof(v) : 0.0078125;   // 1/128 mm: 71 MB grid at C3; fewer EDGE-cell exact tests (fastest on C3)
 }();
 // rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK, multiple of 64)
 int g_jchunk = [] {
