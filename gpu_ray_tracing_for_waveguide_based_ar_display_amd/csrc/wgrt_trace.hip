@@ -1451,6 +1451,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 #endif
 #ifdef WGRT_DIAG
     uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_wait = 0;
+    uint64_t d_free_b = 0, d_transit_b = 0, d_wait_b = 0;   // lane states per pass before the queue ran dry
     const int d_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid] = __builtin_amdgcn_s_memrealtime();
 #endif
@@ -1592,6 +1593,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             if (exhausted) {
                 d_pass_x += 1;
                 d_act_x += na;
+            } else {
+                d_free_b += __popcll(__ballot(!active && !waiting));
+                d_transit_b += __popcll(__ballot(active && blk < 0));
+                d_wait_b += __popcll(__ballot(waiting));
             }
             d_hops += (active && blk == kTransit) ? 1 : 0;
         }
@@ -1665,6 +1670,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         atomicAdd(&g_diag[2], d_pass_x);
         atomicAdd(&g_diag[3], d_act_x);
         atomicAdd(&g_diag[5], d_wait);
+        atomicAdd(&g_diag[13], d_free_b);
+        atomicAdd(&g_diag[14], d_transit_b);
+        atomicAdd(&g_diag[15], d_wait_b);
     }
     d_hops = wave_sum(d_hops);
     if (lane == 0) atomicAdd(&g_diag[4], d_hops);

@@ -63,6 +63,9 @@ print(f"passes={d[0]} mean_active_at_interact={d[1] / max(d[0], 1):.1f}/64 "
       f"passes_after_exhaust={d[2]} ({d[2] / max(d[0], 1):.1%}) mean_active_after={d[3] / max(d[2], 1):.1f}")
 print(f"lane_hops={d[4]} hops/pass(lane-mean)={d[4] / max(d[1], 1):.2f} simt_hop_cost/pass={d[5] / max(d[0], 1):.2f} "
       f"exact_fallbacks={d[16]} interactions~={d[1]} (variants 7-9: d5 = waiting lanes/pass {d[5] / max(d[0], 1):.2f})")
+nb = max(d[0] - d[2], 1)
+print(f"before dry, lanes per pass: interacting={(d[1] - d[3]) / nb:.1f} transit={d[14] / nb:.1f} free={d[13] / nb:.1f} "
+      f"waiting={d[15] / nb:.1f} (variants 7-9)")
 wt = (ctypes.c_ulonglong * (16384 * 3))()
 L.wgrt_diag_read_wave_times.argtypes = [ctypes.POINTER(ctypes.c_ulonglong)]
 L.wgrt_diag_read_wave_times(wt)
