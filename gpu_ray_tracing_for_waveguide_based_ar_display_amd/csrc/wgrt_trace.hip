@@ -203,7 +203,11 @@ __device__ __forceinline__ void diag_region(int r) {
         atomicAdd(&g_diag_act[r], (unsigned long long)__popcll(m));
     }
 }
+#ifdef WGRT_DIAG_LIGHT
+#define DIAG_REGION(r) ((void)0)   // lane-state counters only: no per-region atomics distorting the timing
+#else
 #define DIAG_REGION(r) diag_region(r)
+#endif
 #else
 #define DIAG_REGION(r) ((void)0)
 #endif
@@ -769,6 +773,10 @@ struct JLane {
 
 enum : int { kUncertain = -3, kOut = -4 };
 
+// The Jones-vector lane combines per-lane predicates with & and | on purpose: no short-circuit,
+// so the decision is straight-line code instead of nested divergent branches.
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
+
 // Every column load is issued before anything branches on a loaded value, so a refill waits
 // for one memory round trip (not one for the FoV / wavelength indices and another for the
 // rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
@@ -918,17 +926,18 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
     const double scl = A.cert_tol * fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
     const double tol = scl * cw.w;
-    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic
-    bool ok = tol > 1e-250 && fabs(u - c0) > tol && fabs(u - c1) > tol && (!three || fabs(u - c2) > tol);
+    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic.
+    // Non-short-circuit (&, |) throughout: one straight-line evaluation per lane.
+    bool ok = (tol > 1e-250) & (fabs(u - c0) > tol) & (fabs(u - c1) > tol) & (!three | (fabs(u - c2) > tol));
     const double t = A.threshold;
     bool p0 = true, p1 = true, p2 = true;
-    if (thr) {
-        if (t == 0.0) {
-            // a branch the certified draw selects has e_k > tol (it lies between two thresholds
-            // more than tol from the draw), so ener * e_k > 0 holds for the reference too unless
-            // that product could underflow
-            ok = ok && r.ener * tol > 1e-290;
-        } else {
+    if (t == 0.0) {   // full colour (uniform branch)
+        // a branch the certified draw selects has e_k > tol (it lies between two thresholds more
+        // than tol from the draw), so ener * e_k > 0 holds for the reference too unless that
+        // product could underflow
+        ok = ok & (!thr | (r.ener * tol > 1e-290));
+    } else if (thr) {
+        {
             // ener * e_k > threshold (GRTF:606): certified with ener's tracked relative error
             const double g0 = r.ener * a0, g1 = r.ener * a1, g2 = r.ener * a2;
             const double re = r.eerr + 1e-15;
@@ -943,23 +952,20 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
         }
     }
     ASM_MARK("interact-decide");
-    if (!ok) return kUncertain;
-    int b;
-    if (u <= c0 && p0) b = 0;
-    else if (u <= c1 && p1) b = 1;
-    else if (three && u <= c2 && p2) b = 2;
-    else return kDie;
-
-    if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
-        DIAG_REGION(2);
-        return kOut;   // appended to the out-coupling queue by the caller (at (r.x, r.y))
-    }
-    DIAG_REGION(1);
-    ASM_MARK("interact-take");
-    const bool ba = b == 0;
+    const bool s0 = (u <= c0) & p0;
+    const bool s1 = !s0 & (u <= c1) & p1;
+    const bool s2 = !s0 & !s1 & three & (u <= c2) & p2;   // out-coupling (GRTF:1162-1171, 1231-1240)
+    const bool ba = s0;
     const JField f = ba ? f0 : f1;
     const double n2 = ba ? q0 : q1;
-    if (!(n2 > 1e-300)) return kUncertain;
+    ok = ok & (!(s0 | s1) | (n2 > 1e-300));
+    // one exit for every outcome but a taken branch; an out-coupling is appended to the
+    // out-coupling queue by the caller (at (r.x, r.y))
+    const int code = !ok ? kUncertain : s2 ? kOut : !(s0 | s1) ? kDie : 0;
+    if (code != 0) return code;
+    const int b = ba ? 0 : 1;
+    DIAG_REGION(1);
+    ASM_MARK("interact-take");
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double rn = rsq_nr(n2);
     r.er = f.er * rn;

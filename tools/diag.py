@@ -17,7 +17,8 @@ from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _build, _lib  # n
 import torch  # noqa: E402  (load torch's HIP runtime first, as the package always does)
 torch.cuda.init()
 out = "/tmp/libwgrt_diag.so"
-cmd = [_build._hipcc(), *_build.FLAGS, "-DWGRT_DIAG=1", "-I", os.path.join(REPO, "include"), "-o", out] + \
+cmd = [_build._hipcc(), *_build.FLAGS, "-DWGRT_DIAG=1", *os.environ.get("DIAG_FLAGS", "").split(),
+       "-I", os.path.join(REPO, "include"), "-o", out] + \
       [os.path.join(_build.CSRC, f) for f in _build.SOURCES]
 subprocess.run(cmd, check=True)
 _lib.load(out)
