@@ -493,29 +493,11 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     // provably the reference's decision.  Otherwise -- about once in 1e12 draws -- the lane
     // recomputes every e_k exactly as the reference does.  The chosen branch's magnitudes
     // and efficiency are always computed exactly.
-#ifdef WGRT_EXP_OLD_EST   // experiment: the previous estimate code
-    double q[3];
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        q[k] = 0.0;
-        if (k < 2 || three) {
-            const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
-            q[k] = (f.te_re * f.te_re + f.te_im * f.te_im) + (f.tm_re * f.tm_re + f.tm_im * f.tm_im);
-        }
-    }
-    const double inv = 1.0 / denom;
-#else
     // one branch at a time (a rolled loop keeps the register peak down)
     double q[3] = {0.0, 0.0, 0.0};
     const int nbr = three ? 3 : 2;
-#ifdef WGRT_EXP_UNROLL_SQ
-#pragma unroll
-    for (int k = 0; k < 3; ++k) {
-        if (k >= nbr) break;
-#else
 #pragma unroll 1
     for (int k = 0; k < nbr; ++k) {
-#endif
         const double v = efield_sq(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
         q[0] = k == 0 ? v : q[0];
         q[1] = k == 1 ? v : q[1];
@@ -527,7 +509,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     double inv = __builtin_amdgcn_rcp(denom);
     inv = fma(inv, fma(-denom, inv, 1.0), inv);
     inv = fma(inv, fma(-denom, inv, 1.0), inv);
-#endif
     double a0 = q[0] * B[0] * inv, a1 = q[1] * B[1] * inv;
     if (entry) {
         a0 *= A.n_g;
@@ -1332,11 +1313,6 @@ __device__ __forceinline__ void persistent_body(const TraceArgs &A0, const Loc &
             need = __ballot(!active);
         }
         if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
-#ifdef WGRT_AGE_PRIO
-        // experiment: issue priority for waves carrying old (long-lived) rays
-        if (__ballot(active && L.bounces > (uint32_t)WGRT_AGE_PRIO) != 0ull) __builtin_amdgcn_s_setprio(2);
-        else __builtin_amdgcn_s_setprio(0);
-#endif
 #ifdef WGRT_PHASES
         const uint64_t pt2 = __builtin_amdgcn_s_memtime();
 #endif
