@@ -8,8 +8,10 @@ Same flow as the reference script, on the MI355X kernel:
 3. ray batch: ``num_rays_per_FoV / 2`` in-coupler origins shared by every FoV x wavelength
    block, TE then TM halves (MAIN:59-115), RNG seeds ``0x9E3779B9 * (gid + 1)`` (MAIN:158),
    laid out on the device by ``wgrt_rays_init``;
-4. ``num_iter`` chained launches of the bounce kernel (MAIN:169-177), timed with HIP events
-   (no JIT in the timed region, unlike the reference's wall clock);
+4. ``num_iter`` chained launches of the bounce kernel (MAIN:169-177), by default as one fused
+   call (``num_iter`` traces per ray in one persistent launch; identical results; ``fuse=False``
+   issues separate launches), timed with HIP events (no JIT in the timed region, unlike the
+   reference's wall clock);
 5. efficiencies ``A = sum(EB) / N / num_iter``, ``eff_c = 3 * sum(A[lambda])`` (MAIN:186-192)
    and ``evaluation(EB / R / num_iter)`` (MAIN:197-198).
 
@@ -29,13 +31,14 @@ import numpy as np
 
 def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000, num_iter: int = 4,
         lambdas=(0, 1, 2), lut_dir: str | None = None, lut_seed: int = 0, lut_profile: str = "default",
-        point_seed: int | None = None, evaluate: bool = True, verbose: bool = True, variant: int = 0) -> dict:
+        point_seed: int | None = None, evaluate: bool = True, verbose: bool = True, variant: int = 0,
+        fuse: bool = True) -> dict:
     import torch
     import torch.distributed as dist
 
     from .couplers_coor import design_geometry
     from .distributed import make_shard, reduce_eyebox
-    from .engine import Scene, init_rays, trace_fullcolor
+    from .engine import Scene, init_rays, reserve, trace_fullcolor
     from .luts import load_luts, synthetic_luts, validate_luts
     from .rays import generate_points_in_polygon
 
@@ -69,11 +72,19 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     num_rays = num_FOV_x * num_FOV_y * len(lambdas) * R
     say(f"Initialization complete: {num_rays:,} rays, {world} GPU(s)\n" + "=" * 60 + "\nSTART GPU RAY TRACING\n" + "=" * 60)
 
+    # the num_iter chained launches of MAIN:169-177; fuse: as one call (wgrt_launch_opts.num_iter,
+    # one persistent launch for the Jones-vector variants), with results identical to num_iter calls
+    calls = [1] * num_iter
+    if fuse:   # at most 255 traces per call (wgrt_launch_opts.num_iter)
+        calls = [min(255, num_iter - k) for k in range(0, num_iter, 255)]
+    if shard.n_rays and calls:
+        reserve(scene, shard.n_rays, max(calls))
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0.record()
-    for _ in range(num_iter):
+    for k in calls:
         if shard.n_rays:
-            trace_fullcolor(scene, rays, rng, eb, gid_offset=shard.gid_offset, stats=stats, variant=variant)
+            trace_fullcolor(scene, rays, rng, eb, gid_offset=shard.gid_offset, stats=stats, variant=variant,
+                            num_iter=k)
     t1.record()
     torch.cuda.synchronize()
     kern_s = t0.elapsed_time(t1) / 1e3
@@ -118,6 +129,7 @@ def main(argv=None):
     ap.add_argument("--lut-profile", default="default")
     ap.add_argument("--point-seed", type=int, default=None)
     ap.add_argument("--no-eval", action="store_true")
+    ap.add_argument("--no-fuse", action="store_true", help="issue num_iter separate launches")
     ap.add_argument("--json", default=None, help="write scalar results here")
     a = ap.parse_args(argv)
     import torch
@@ -127,7 +139,7 @@ def main(argv=None):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     res = run(a.num_fov_x, a.num_fov_y, a.rays_per_fov, a.num_iter, lut_dir=a.lut_dir, lut_seed=a.lut_seed,
-              lut_profile=a.lut_profile, point_seed=a.point_seed, evaluate=not a.no_eval)
+              lut_profile=a.lut_profile, point_seed=a.point_seed, evaluate=not a.no_eval, fuse=not a.no_fuse)
     if a.json and (not dist.is_initialized() or dist.get_rank() == 0):
         keep = {k: v for k, v in res.items() if isinstance(v, (int, float, dict, str))}
         with open(a.json, "w") as f:
