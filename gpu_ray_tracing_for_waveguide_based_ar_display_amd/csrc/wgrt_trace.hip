@@ -64,12 +64,6 @@ int g_jchunk = [] {
     const int c = v ? atoi(v) : 64;
     return c >= 64 ? c / 64 * 64 : 64;
 }();
-// miss hops per pass of the Jones-vector variants (env WGRT_JMAX_HOPS; 1 measured best on C3:
-// every hop then tests a cell word loaded at least a pass earlier)
-int g_jmax_hops = [] {
-    const char *v = getenv("WGRT_JMAX_HOPS");
-    return v ? atoi(v) : 1;
-}();
 double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
 int g_max_hops = [] {
     const char *v = getenv("WGRT_MAX_HOPS");
@@ -974,15 +968,17 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 }
 
 // Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
-// that need no Monte-Carlo interaction, at most A.max_hops per call (1 by default: every
-// iteration then tests a cell word loaded a pass earlier, L.pf, and a hop issues the load of
-// the next one).
+// that need no Monte-Carlo interaction, at most kJMaxHops per call: every iteration then tests
+// a cell word loaded a pass earlier, L.pf, and a hop issues the load of the next one.  1 measured
+// best on C3 (2 and 4 slower); a compile-time bound, not a kernarg, straightens the loop (-2 %
+// fused).
+constexpr int kJMaxHops = 1;
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     JRay &r = L.r;
     ASM_MARK("advance");
     for (int hops = 0;; ++hops) {
-        if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
+        if (hops >= kJMaxHops) return kTransit;
         DIAG_REGION(3);
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
@@ -1502,7 +1498,23 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         const uint64_t pt1 = __builtin_amdgcn_s_memtime();
 #endif
         ASM_MARK("refill");
-        if (FUSED && waiting) start();   // poll the previous trace's granule again
+        if (FUSED && waiting) {
+            // poll only the previous trace's granule: the ray's columns are still in L from the
+            // start() that found it not ready
+            const uint64_t w = __hip_atomic_load(KA(rng64) + L.i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint32_t tag = (uint32_t)w;
+            if (tag == iter_tag(A.iter_epoch, L.k, false)) {
+                L.r.s = (uint32_t)(w >> 32);
+                L.s0 = L.r.s;
+                waiting = false;
+                active = true;
+                blk = 0;
+                kind = 0;
+                entry = true;
+            } else if ((tag >> 8) == ((A.iter_epoch << 1) | 1u)) {
+                waiting = false;   // abandoned in an earlier iteration: the replay kernel finishes it
+            }
+        }
         uint64_t need = __ballot(!active && !waiting);
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
@@ -2152,7 +2164,7 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
         HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
         const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
-        A.max_hops = g_jmax_hops;
+        A.max_hops = kJMaxHops;   // informational: the Jones loop has it compiled in
         LocatorT<uint32_t> l32;
         l32.cells = s->d_cells32;
         l32.verts = A.loc.verts;
