@@ -5,28 +5,30 @@ BASELINE.json metric: "ray-bounces/sec, full-color 21x21 FoV, num_rays_per_FoV=1
 1/2/4/8 GPU".  A ray-bounce = 1 in-coupling event + 1 per executed iteration of the
 reference's bounce loop (GRTF:860-905); counted on the device by the kernel itself.
 
-One step = one trace of every ray of the per-rank batch = one of the reference's
-``num_iter`` chained launches (gpu_ray_tracing_pro_fullColor.py:169-177): each step starts
-from the RNG states the previous one left and adds its out-couplings to the eyebox grid.
-By default the K timed steps run as ONE fused launch (``num_iter = K``, wgrt_launch_opts):
-every ray is traced K times in order inside one persistent kernel, so one step's straggler
-tail overlaps the next step's bulk; results (RNG states, eyebox grid, bounce counts) are
-bit-identical to K separate launches (tests/test_gpu_parity.py::test_fused_iterations_*).
-``--fuse 1`` times K separate launches instead; the JSON line reports that rate too
-(``unfused``).  At N > 1 the eyebox grid is RCCL-reduced to rank 0 after the steps.
-Inputs (ray SoA, RNG, scene) are resident in HBM before timing starts.
+One step = one trace of every ray of the batch = ONE launch of the reference's kernel
+(gpu_ray_tracing_pro_fullColor.py:169-177 issues num_iter = 4 of them, each starting from
+the RNG states the previous one left and adding its out-couplings to the eyebox grid).  The
+headline ``value`` times K such steps as K separate launches (``num_iter = 1`` each, SURVEY.md
+§8(d)), inputs already resident in HBM, plus the RCCL reduce of the eyebox grid at N > 1.
+Two more rates of the same batch ride along: ``main_job`` -- the reference's job shape, 4
+chained traces issued as one call (the engine fuses them into one persistent launch,
+bit-identical to 4 launches) -- and ``fused`` -- all K steps in one call.
 
-Multi-GPU (weak scaling): the job at N GPUs traces num_rays_per_FoV = 1024 * N rays per
-FoV x wavelength block and shards the blocks (contiguous global-ray ranges) over the
-ranks, so every rank traces 21 x 21 x 3 x 1024 rays per step, with its global ray ids
-(RNG seeds are global, results independent of N).  Launch:
+Workloads (``--config``, BASELINE.json configs):
+    C3  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 1024           (1 GPU)
+    C4  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 4096, sharded  (N GPUs)
+    C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce LUT, sharded
+    auto (default): C3 at N = 1, C4 at N > 1 (BASELINE's multi-GPU config); sharded configs
+    split the FoV x wavelength blocks over the ranks (total work fixed: "strong" scaling).
+Multi-GPU: one process per GPU through distributed.py (the same sharding / stepping / reduce
+code the reference-flow driver uses):
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 """
 from __future__ import annotations
 
 import argparse
+import hashlib
 import json
-import math
 import os
 import sys
 import time
@@ -39,42 +41,62 @@ sys.path.insert(0, REPO)
 ALGO_BYTES_PER_BOUNCE = 72      # read + write of the minimal 36-B ray record
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 
+CONFIGS = {
+    "C3": dict(nx=21, ny=21, lambdas=(0, 1, 2), R=1024, profile="default",
+               name="BASELINE config 3: full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV=1024"),
+    "C4": dict(nx=21, ny=21, lambdas=(0, 1, 2), R=4096, profile="default",
+               name="BASELINE config 4: full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV=4096, FoV x lambda sharded"),
+    "C5": dict(nx=41, ny=41, lambdas=(0, 1, 2), R=16384, profile="deep",
+               name="BASELINE config 5: full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV=16384, deep-bounce LUT, "
+                    "FoV x lambda sharded"),
+}
 
-def parse():
+
+def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--nx", type=int, default=21)
-    ap.add_argument("--ny", type=int, default=21)
-    ap.add_argument("--rays-per-fov", type=int, default=1024, help="per GPU (weak scaling)")
-    ap.add_argument("--lambdas", default="0,1,2")
-    ap.add_argument("--lut-profile", default="default")
+    ap.add_argument("--config", default="auto", choices=["auto", "C3", "C4", "C5"])
     ap.add_argument("--lut-seed", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
-    ap.add_argument("--workgroups", type=int, default=0)
-    ap.add_argument("--fuse", type=int, default=0,
-                    help="steps per launch (0: all timed steps in one fused launch, at most 255)")
-    ap.add_argument("--no-unfused", action="store_true", help="skip the separate-launch comparison")
+    ap.add_argument("--no-extras", action="store_true", help="skip the main_job / fused rates")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
-    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "hbm_traffic.json"),
-                    help="PMC-derived HBM bytes per launch (written by tools/pmc_traffic.py)")
-    return ap.parse_args()
+    ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
+                    help="PMC traffic per bounce (tools/pmc_traffic.py), used when its library hash matches")
+    return ap.parse_args(argv)
 
 
-def main():
-    a = parse()
+def config_for(name: str, world: int) -> tuple[str, dict]:
+    if name == "auto":
+        name = "C3" if world == 1 else "C4"
+    return name, CONFIGS[name]
+
+
+def metric_name(cfg: dict) -> str:
+    return (f"ray-bounces/sec, full-color {cfg['nx']}x{cfg['ny']} FoV, num_rays_per_FoV={cfg['R']}"
+            + ("" if cfg["profile"] == "default" else f", {cfg['profile']}-bounce LUT"))
+
+
+def lib_sha16() -> str:
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd._lib import LIB_PATH
+    with open(LIB_PATH, "rb") as f:
+        return hashlib.sha256(f.read()).hexdigest()[:16]
+
+
+def main(argv=None):
+    a = parse(argv)
     import torch
     import torch.distributed as dist
 
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import block_range, reduce_eyebox
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, rays_to_device, reserve,
-                                                                           trace_fullcolor)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
+                                                                                make_shard, reduce_eyebox,
+                                                                                run_steps, split_calls)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, reserve
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import (build_rays, generate_points_in_polygon,
-                                                                         rng_seeds)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
@@ -86,162 +108,148 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=dev)
 
-    lambdas = [int(v) for v in a.lambdas.split(",")]
-    nx, ny = a.nx, a.ny
-    R = a.rays_per_fov * world                 # global rays per FoV x lambda block
-    nblk = nx * ny * len(lambdas)
-    lo, hi = block_range(nblk, world, rank)
+    cname, cfg = config_for(a.config, world)
+    nx, ny, lambdas, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
     geom = design_geometry(nx, ny)
-    luts = synthetic_luts(geom, seed=a.lut_seed, profile=a.lut_profile)
-    points = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
-    host_rays = build_rays(points, nx, ny, lambdas, R, blocks=(lo, hi))
-    n_local = host_rays["x"].shape[0]
-    gid0 = lo * R
+    luts = synthetic_luts(geom, seed=a.lut_seed, profile=cfg["profile"])
+    points = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))   # same on every rank
+    t_scene = time.perf_counter()
     scene = Scene.from_geometry(geom, luts, device=local)
-    rays = rays_to_device(host_rays, dev)
-    seeds = rng_seeds(n_local, gid0)
-    rng = torch.from_numpy(seeds.view(np.int32)).to(dev)
+    t_scene = time.perf_counter() - t_scene
+    shard = make_shard(nx, ny, len(lambdas), R, world, rank)
+    rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard.block_lo, shard.block_hi)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    tracer = hip_tracer(scene, a.variant, stats)
+    reserve(scene, shard.n_rays, max(split_calls(max(a.steps, 4), 0)))
 
-    def launches(steps, fuse):
-        """split `steps` steps into launches of at most `fuse` steps (0: as few as possible)"""
-        f = min(255, steps if fuse <= 0 else fuse)
-        out = []
-        while steps > 0:
-            out.append(min(f, steps))
-            steps -= out[-1]
-        return out
-
-    def run(steps, fuse, events=None):
-        for j, k in enumerate(launches(steps, fuse)):
-            if events is not None:
-                events[j][0].record()
-            trace_fullcolor(scene, rays, rng, eb, gid_offset=gid0, stats=stats, variant=a.variant,
-                            workgroups=a.workgroups, num_iter=k)
-            if events is not None:
-                events[j][1].record()
-
-    def timed(steps, fuse):
+    def timed(steps, per_call):
+        """steps chained traces as calls of per_call traces; HIP events around every call on the
+        stream the kernels run on (torch's current stream, where engine launches them)."""
         stats.zero_()
-        events = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-                  for _ in launches(steps, fuse)]
+        ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+              for _ in split_calls(steps, per_call)]
+        hook = lambda j, what: ev[j][0 if what == "start" else 1].record()
         if world > 1:
             dist.barrier()
         torch.cuda.synchronize()
         t0 = time.perf_counter()
-        run(steps, fuse, events)
+        run_steps(tracer, rays, rng, eb, shard.gid_offset, steps, per_call, hook)
         if world > 1:
             reduce_eyebox(eb)
         torch.cuda.synchronize()
         if world > 1:
             dist.barrier()
         elapsed = time.perf_counter() - t0
-        kern_ms = [s.elapsed_time(e) for s, e in events]
-        bounces_local = int(stats[0].item())
+        call_ms = [s.elapsed_time(e) for s, e in ev]
+        b_local = int(stats[0].item())
         t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        b = torch.tensor([bounces_local], dtype=torch.int64, device=dev)
+        b = torch.tensor([b_local], dtype=torch.int64, device=dev)
         if world > 1:
             dist.all_reduce(t, op=dist.ReduceOp.MAX)
             dist.all_reduce(b, op=dist.ReduceOp.SUM)
-        return float(t.item()), int(b.item()), bounces_local, kern_ms
+        return float(t.item()), int(b.item()), b_local, call_ms
 
-    # warm-up: W separate launches (the fused kernel then appears in a kernel trace only with
-    # the timed launches, so its average duration there is the timed one), scratch reserved for
-    # the timed launches' sizes
-    reserve(scene, n_local, launches(a.steps, a.fuse)[0])
-    run(a.warmup, 1)
+    # warm-up: W separate launches (and one fused call, so the fused kernels are loaded too)
+    run_steps(tracer, rays, rng, eb, shard.gid_offset, a.warmup, 1)
+    if not a.no_extras:
+        run_steps(tracer, rays, rng, eb, shard.gid_offset, 2, 0)
     torch.cuda.synchronize()
-    elapsed, bounces_total, bounces_local, kern_ms = timed(a.steps, a.fuse)
+    elapsed, bounces_total, bounces_local, call_ms = timed(a.steps, 1)
     value = bounces_total / elapsed
-    unfused = None
-    if not a.no_unfused and a.fuse != 1:
-        u_el, u_b, _, u_ms = timed(a.steps, 1)
-        unfused = {"value": round(u_b / u_el, 1), "ms_per_step": round(u_el / a.steps * 1e3, 4),
-                   "kernel_avg_ms": round(float(np.mean(u_ms)), 4),
-                   "note": "the same K steps as K separate launches (num_iter = 1 each)"}
+    extras = {}
+    if not a.no_extras:
+        for key, steps, note in (("main_job", 4, "the reference's job: 4 chained traces (MAIN:169-177) as one call, "
+                                                 "fused into one persistent launch"),
+                                 ("fused", a.steps, f"the same {a.steps} steps as one call (one persistent launch)")):
+            e_el, e_b, e_bl, e_ms = timed(steps, 0)
+            extras[key] = {"value": round(e_b / e_el, 1), "ms_per_step": round(e_el / steps * 1e3, 4),
+                           "steps": steps, "kernel_avg_ms": round(float(np.mean(e_ms)), 4), "note": note}
 
     if rank == 0:
-        steps_per_launch = launches(a.steps, a.fuse)[0]
-        kavg_s = float(np.mean(kern_ms)) / 1e3
-        bounces_per_launch_local = bounces_local / len(kern_ms)
-        achieved = bounces_per_launch_local * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
-        cfg_key = f"{nx}x{ny}x{len(lambdas)}xR{a.rays_per_fov}:{a.lut_profile}:{a.lut_seed}:v{a.variant}"
-        traffic = None
+        kavg_s = float(np.mean(call_ms)) / 1e3
+        achieved = bounces_local / len(call_ms) * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
+        sha = lib_sha16()
+        traffic, traffic_note = None, "no PMC pass recorded for this library build"
         try:
             with open(a.traffic_json) as f:
-                per_bounce = json.load(f).get(cfg_key, {}).get("hbm_bytes_per_bounce")
-            if per_bounce is not None:
-                traffic = int(round(per_bounce * bounces_per_launch_local))
-        except (OSError, ValueError):
+                ent = json.load(f).get(f"{cname}:v{a.variant}")
+            if ent and ent.get("lib_sha16") == sha:
+                traffic = int(round(ent["bytes_per_bounce"] * bounces_local / len(call_ms)))
+                traffic_note = ("rocprofv3 FETCH_SIZE + WRITE_SIZE of the trace kernel on this build (L2 <-> fabric "
+                                "bytes; Infinity-Cache hits included, so an upper bound on HBM bytes), per launch")
+        except (OSError, ValueError, KeyError):
             pass
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic,
-                    "kernel": kernel_name(a.variant, scene, steps_per_launch > 1),
-                    "kernel_avg_ms": round(kavg_s * 1e3, 4), "steps_per_launch": steps_per_launch,
+                    "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_note": traffic_note,
+                    "kernel": kernel_name(a.variant, scene), "launch_avg_ms": round(kavg_s * 1e3, 4),
                     "algo_bytes_per_bounce": ALGO_BYTES_PER_BOUNCE,
-                    "bounces_per_launch": int(round(bounces_per_launch_local))}
+                    "bounces_per_launch": int(round(bounces_local / len(call_ms))),
+                    "note": "launch_avg_ms: HIP events around each launch (trace kernel + its eyebox/replay "
+                            "epilogue kernels) on rank 0"}
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(geom, luts, points, nx, ny, lambdas, R, a.cpu_seconds)
         line = {
-            "metric": "ray-bounces/sec, full-color 21x21 FoV, num_rays_per_FoV=1024",
+            "metric": metric_name(cfg),
             "value": round(value, 1), "unit": "ray-bounces/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
-            "config": {"workload": f"full-colour {nx}x{ny} FoV x {len(lambdas)} lambda, "
-                                   f"num_rays_per_FoV={a.rays_per_fov} per GPU (BASELINE config 3)",
-                       "nx": nx, "ny": ny, "lambdas": lambdas, "rays_per_fov_per_gpu": a.rays_per_fov,
-                       "rays_per_gpu": n_local, "lut": f"synthetic seed {a.lut_seed} profile {a.lut_profile}",
-                       "geometry": "couplers_coor_full_color restatement",
+            "scaling": "strong", "vs_baseline": None, "dtype": "f64",
+            "data": "synthetic (seeded LUT and ray origins; geometry from the couplers_coor restatement)",
+            "config": {"workload": f"{cname}: {cfg['name']}", "nx": nx, "ny": ny, "lambdas": lambdas,
+                       "num_rays_per_FoV": R, "rays_total": nx * ny * len(lambdas) * R, "rays_rank0": shard.n_rays,
+                       "lut": f"synthetic seed {a.lut_seed} profile {cfg['profile']}",
                        "parallelism": f"fov-lambda block shards x{world}" + (" + RCCL reduce(EB)" if world > 1 else ""),
-                       "kernel_variant": a.variant,
-                       "steps_per_launch": steps_per_launch},
+                       "kernel_variant": a.variant, "steps_per_launch": 1, "lib_sha16": sha,
+                       "scene_create_s": round(t_scene, 3)},
             "roofline": roofline,
-            "unfused": unfused,
+            "main_job": extras.get("main_job"),
+            "fused": extras.get("fused"),
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
+    scene.close()
     if world > 1:
         dist.destroy_process_group()
 
 
-def kernel_name(variant, scene, fused=False):
-    """Name of the kernel a launch runs (wgrt_trace_fullcolor_ex's variant table; auto = 7
-    when the scene has <= 16 polygons, else 9; a fused launch of variant 7 or 8 runs the
-    fused variant-7 kernel)."""
+def kernel_name(variant, scene):
+    """Name of the kernel a single-trace launch runs (include/wgrt.h's variant table: auto = 7
+    when the scene has <= 16 polygons, else 9)."""
     if variant == 0:
         variant = 7 if scene.info()["n_polygons"] <= 16 else 9
-    if fused and variant >= 7:
-        return "trace_jones_kernel<unsigned %s, 3, true>" % ("long" if variant == 9 else "int")
-    return {1: "trace_grid_kernel", 2: "trace_persistent_kernel", 3: "trace_persistent_lds_kernel",
-            4: "trace_persistent_g_kernel<unsigned long, 4>", 5: "trace_persistent_g_kernel<unsigned int, 3>",
-            6: "trace_persistent_g_kernel<unsigned int, 4>", 7: "trace_jones_kernel<unsigned int, 3>",
-            8: "trace_jones_kernel<unsigned int, 4>", 9: "trace_jones_kernel<unsigned long, 3>"}[variant]
+    return {1: "trace_grid_kernel", 7: "trace_jones_kernel<unsigned int, false>",
+            9: "trace_jones_kernel<unsigned long, false>"}[variant]
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):
-    """Time the CPU oracle (oracle/wgrt_oracle.c, float64, OpenMP) on the same workload:
-    chained launches over the whole batch (like the reference's num_iter loop, MAIN:169)
-    until ~target_s seconds of wall time have been spent."""
+    """Time the CPU oracle (oracle/wgrt_oracle.c, float64, OpenMP) on a bounded sample of the
+    same workload: successive slices of FoV x wavelength blocks (64 blocks each, wrapping
+    around with chained RNG states) until ~target_s seconds of wall time have been spent."""
     from oracle import OracleScene
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
     threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
     threads = min(threads, os.cpu_count() or threads)
     sc = OracleScene.from_geometry(geom, luts)
     nblk = nx * ny * len(lambdas)
-    rays = build_rays(points, nx, ny, lambdas, R, blocks=(0, nblk))
-    rng = rng_seeds(rays["x"].shape[0])
+    per = min(64, nblk)
     eb = np.zeros(sc.eb_shape(), np.float32)
-    tot, dt, launches = 0, 0.0, 0
-    while dt < target_s and launches < 256:
+    tot, dt, n_rays, k = 0, 0.0, 0, 0
+    slices = {}
+    while dt < target_s and k < 4096:
+        lo = (k * per) % nblk
+        hi = min(lo + per, nblk)
+        if lo not in slices:
+            slices[lo] = (build_rays(points, nx, ny, lambdas, R, blocks=(lo, hi)), rng_seeds((hi - lo) * R, lo * R))
+        rays, rng = slices[lo]
         t = time.perf_counter()
-        b, _ = sc.trace(rays, rng, eb, threads=threads)
+        b, _ = sc.trace(rays, rng, eb, gid_offset=lo * R, threads=threads)
         dt += time.perf_counter() - t
         tot += b
-        launches += 1
+        n_rays += (hi - lo) * R
+        k += 1
     return {"value": round(tot / dt, 1), "unit": "ray-bounces/s", "cores": threads, "kind": "port",
-            "sample": f"{launches} chained launches over the full batch ({nblk} FoV x lambda blocks x {R} rays; "
+            "sample": f"{k} traces of {per}-block slices ({n_rays} rays of {nblk} FoV x lambda blocks x {R}; "
                       f"{tot} bounces in {dt:.2f} s); oracle/wgrt_oracle.c float64 OpenMP, {threads} threads"}
 
 

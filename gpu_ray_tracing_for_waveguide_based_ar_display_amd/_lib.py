@@ -14,7 +14,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libwgrt.so")
 
-ABI_VERSION = 1
+ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_status_string",
@@ -69,7 +69,7 @@ class SceneInfo(ctypes.Structure):
                 ("grid_cells_x", ctypes.c_int64), ("grid_cells_y", ctypes.c_int64),
                 ("grid_cell_mm", ctypes.c_double), ("grid_edge_cells", ctypes.c_int64),
                 ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("lds_locator_bytes", ctypes.c_int64), ("lds_cell_mm", ctypes.c_double)]
+                ("jtile_bytes", ctypes.c_int64)]
 
 
 _lib = None
@@ -113,8 +113,7 @@ def load(path: str = LIB_PATH):
     L.wgrt_scene_classify.restype = st
     L.wgrt_scene_classify.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_locator_classify_host.restype = st
-    L.wgrt_locator_classify_host.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_double, ctypes.c_int, _vp,
-                                             ctypes.c_int64, _vp]
+    L.wgrt_locator_classify_host.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_double, _vp, ctypes.c_int64, _vp]
     L.wgrt_selftest_math.restype = st
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
@@ -263,7 +262,7 @@ class Scene:
             pass
 
 
-def locator_classify_host(geom, luts, xy: np.ndarray, cell_mm: float = 0.125, which: int = 0) -> np.ndarray:
+def locator_classify_host(geom, luts, xy: np.ndarray, cell_mm: float = 0.125) -> np.ndarray:
     """Host replica of the kernels' polygon locator (``wgrt_locator_classify_host``): bit k of
     the result is is_inside_or_on_edge(point, polygon k) (0 eff_reg1, 1 eff_reg2, 2 IC,
     3.. FC slices, then OC slices).  Needs no GPU."""
@@ -274,7 +273,7 @@ def locator_classify_host(geom, luts, xy: np.ndarray, cell_mm: float = 0.125, wh
                               luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"], geom.lut_TIR, geom.lut_gap)
     pts = np.ascontiguousarray(xy, dtype=np.float64)
     out = np.zeros(pts.shape[0], dtype=np.uint64)
-    check(L.wgrt_locator_classify_host(ctypes.byref(desc), float(cell_mm), int(which),
-                                       pts.ctypes.data_as(_vp), pts.shape[0], out.ctypes.data_as(_vp)),
+    check(L.wgrt_locator_classify_host(ctypes.byref(desc), float(cell_mm), pts.ctypes.data_as(_vp), pts.shape[0],
+                                       out.ctypes.data_as(_vp)),
           "wgrt_locator_classify_host")
     return out

@@ -41,7 +41,6 @@ namespace {
 
 constexpr double kPad = 1e-6;          // mm; >> tol (1e-12) and >> float64 rounding at |x| ~ 60 mm
 constexpr double kShortEdge = 1e-4;    // mm; shorter edges use the bbox criterion
-constexpr size_t kLdsBudget = 150 * 1024;  // bytes of LDS a workgroup may spend on the locator
 
 struct Poly {
     const double *xy;
@@ -396,49 +395,6 @@ void validate_desc(const wgrt_scene_desc &d) {
     check(d.n_oc_slices == 0 || d.OC_offset[0] >= 0, "OC_offset[0] < 0");
 }
 
-namespace {
-size_t align16(size_t v) { return (v + 15) & ~(size_t)15; }
-}  // namespace
-
-bool build_lds_image(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
-                     double cell_mm, size_t max_bytes, LdsImage &out) {
-    out = LdsImage();
-    if (polys.size() > 16) return false;
-    for (double h = cell_mm; h <= 64 * cell_mm; h *= 2) {
-        LocatorHost L;
-        build_locator(polys, nverts, h, L);
-        const size_t v = L.verts.size() * sizeof(double);
-        const size_t c = L.cells.size() * sizeof(uint32_t);
-        const size_t po = L.poly_off.size() * sizeof(int32_t);
-        const size_t ro = L.row_off.size() * sizeof(int32_t);
-        const size_t re = L.row_edges.size() * sizeof(int32_t);
-        const size_t o_cells = align16(v), o_poly = o_cells + align16(c), o_row = o_poly + align16(po);
-        const size_t o_edges = o_row + align16(ro), total = o_edges + align16(re);
-        if (total > max_bytes) continue;
-        out.bytes.assign(total, 0);
-        std::memcpy(out.bytes.data(), L.verts.data(), v);
-        uint32_t *cells = reinterpret_cast<uint32_t *>(out.bytes.data() + o_cells);
-        for (size_t k = 0; k < L.cells.size(); ++k) cells[k] = (uint32_t)L.cells[k];
-        std::memcpy(out.bytes.data() + o_poly, L.poly_off.data(), po);
-        std::memcpy(out.bytes.data() + o_row, L.row_off.data(), ro);
-        if (re) std::memcpy(out.bytes.data() + o_edges, L.row_edges.data(), re);
-        out.off_verts = 0;
-        out.off_cells = (int)o_cells;
-        out.off_poly = (int)o_poly;
-        out.off_row_off = (int)o_row;
-        out.off_row_edges = (int)o_edges;
-        out.x0 = L.x0;
-        out.y0 = L.y0;
-        out.h = L.h;
-        out.inv_h = L.inv_h;
-        out.ncx = L.ncx;
-        out.ncy = L.ncy;
-        out.ok = true;
-        return true;
-    }
-    return false;
-}
-
 void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) {
     validate_desc(d);
     std::vector<const double *> polys;
@@ -458,7 +414,6 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) 
         nv.push_back(d.OC_offset[k + 1] - d.OC_offset[k]);
     }
     build_locator(polys, nv, cell_mm, out.loc);
-    build_lds_image(polys, nv, 2 * cell_mm, kLdsBudget, out.lds);
     pack_tiles(d, out.tiles);
     pack_jtiles(d, out.tiles, out.jtiles);
     // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would

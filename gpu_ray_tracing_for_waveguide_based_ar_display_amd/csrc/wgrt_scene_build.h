@@ -29,19 +29,8 @@ struct LocatorHost {
     int64_t edge_cells = 0;
 };
 
-// Byte image of a locator with 32-bit cell words (<= 16 polygons) for LDS staging:
-// [verts f64 | cells u32 | poly_off i32 | row_off i32 | row_edges i32], 16-B aligned parts.
-struct LdsImage {
-    std::vector<char> bytes;
-    int off_cells = 0, off_verts = 0, off_poly = 0, off_row_off = 0, off_row_edges = 0;
-    double x0 = 0, y0 = 0, h = 0, inv_h = 0;
-    int ncx = 0, ncy = 0;
-    bool ok = false;
-};
-
 struct SceneHost {
     LocatorHost loc;
-    LdsImage lds;
     std::vector<double> tiles;     // [num_lmd * nx * ny][tile_doubles]
     int tile_doubles = 0;
     std::vector<double> jtiles;    // [num_lmd * nx * ny][jtile_doubles] (Jones-vector variants)
@@ -54,8 +43,5 @@ void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles);
 void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std::vector<double> &jtiles);
 void validate_desc(const wgrt_scene_desc &d);
 void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out);
-// Largest-resolution locator image (cell size cell_mm * 2^k) that fits in max_bytes.
-bool build_lds_image(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
-                     double cell_mm, size_t max_bytes, LdsImage &out);
 
 }  // namespace wgrt

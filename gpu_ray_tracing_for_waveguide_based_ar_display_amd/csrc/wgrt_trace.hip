@@ -2,25 +2,20 @@
 // and the C ABI declared in include/wgrt.h.
 //
 // Restates the reference's full-colour kernel process_rays_kernel_pro_fullColor
-// (GPU_ray_tracing_functions.py = GRTF:833-1246, call at gpu_ray_tracing_pro_fullColor.py:170).
-// One ray per lane (wave64); the ray record lives in VGPRs for its whole life; the
-// only global writes are the final RNG state, optional per-ray bounce counts, one
-// float atomic per eyebox hit (GRTF:164) and one set of 64-bit stats atomics per
-// workgroup.
+// (GPU_ray_tracing_functions.py = GRTF:833-1246, call at gpu_ray_tracing_pro_fullColor.py:170)
+// and its single-wavelength twin process_rays_kernel_pro (GRTF:419-831).  One ray per lane
+// (wave64); the ray record lives in VGPRs for its whole life; the only global writes are the
+// final RNG state, optional per-ray bounce counts, one float atomic per eyebox hit (GRTF:164)
+// and one set of 64-bit stats atomics per wave.
 //
-// Arithmetic is float64 throughout, like the reference (its state is promoted to
-// float64 on first use, GRTF:846-882), compiled with -ffp-contract=off and in the
-// reference's expression order, so results match the reference bit for bit except
-// where the device libm's cos/sin/atan2 differ from glibc's in the last ulp -- which
-// changes a Monte-Carlo decision only if a uniform draw lands within ~1e-16 of a
-// branch threshold.
-//
-// Kernel structure: the reference's six-state machine (R0..R5)
-// is driven by data.  Every coupler interaction, whatever its state, runs the same
-// instruction stream: fetch one "interaction block" of the per-(lambda, FoV) LUT tile
-// (2 or 3 Jones matrices + cosines), evaluate the branch efficiencies, draw, pick the
-// branch, and only then evaluate the atan2 phase of the chosen branch.  The six states
-// therefore diverge only in the short polygon-scan / hop code, not in the fp64 math.
+// Two lanes implement the reference's per-ray state machine (R0..R5):
+//   * the exact lane (variant 1, the replay kernel, the diagnostic shadow): the reference's
+//     float64 arithmetic in its expression order (E_field_cal with correctly rounded hypot,
+//     GRTF:132-152), compiled with -ffp-contract=off;
+//   * the Jones-vector lane (variants 7 / 9, the product path): the same decisions from the
+//     field carried as a complex Jones vector, each certified against a bound on the
+//     difference to the exact arithmetic; an uncertain decision abandons the ray, which the
+//     replay kernel re-traces with the exact lane.
 // Polygon membership goes through the exact grid locator (wgrt_scene_build.cpp).
 #include <hip/hip_runtime.h>
 
@@ -39,21 +34,12 @@
 #include "wgrt_common.h"
 #include "wgrt_scene_build.h"
 
-#ifndef WGRT_W8
-#define WGRT_W8 4   // waves per SIMD of variant 8
-#endif
-
 using namespace wgrt;
 
 namespace {
 
 thread_local std::string g_last_error;
-// Miss hops a lane may take per pass of the persistent loop before the wave's interaction
-// step (env WGRT_MAX_HOPS, 0 = unbounded).  Bounding it keeps lanes whose ray is crossing a
-// coupler-free stretch from stalling the whole wave; 2 measured best on the C3 workload
-// (0.92 ms vs 1.05 ms unbounded, tools/ab.py).  Scheduling only: results are identical.
-// Cell size (mm) of the global-memory locator grid (env WGRT_CELL_MM); the LDS copy uses
-// the smallest power-of-two multiple of twice this size that fits the LDS budget.
+// Cell size (mm) of the global-memory locator grid (env WGRT_CELL_MM).
 double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
     return v ? atof(v) : 0.0078125;   // 1/128 mm: 71 MB grid at C3; fewer EDGE-cell exact tests (fastest on C3)
@@ -65,10 +51,6 @@ int g_jchunk = [] {
     return c >= 64 ? c / 64 * 64 : 64;
 }();
 double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
-int g_max_hops = [] {
-    const char *v = getenv("WGRT_MAX_HOPS");
-    return v ? atoi(v) : 2;
-}();
 
 wgrt_status fail(wgrt_status s, const std::string &msg) {
     g_last_error = msg;
@@ -85,8 +67,8 @@ wgrt_status fail(wgrt_status s, const std::string &msg) {
 // ----------------------------------------------------------------------------
 // device-side scene view
 // ----------------------------------------------------------------------------
-// The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t for the global-memory
-// copy (up to 32 polygons), uint32_t for the LDS-resident copy (up to 16 polygons).
+// The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t cell words (up to 32
+// polygons), uint32_t (up to 16 polygons: half the grid's cache footprint).
 template <class CellT>
 struct LocatorT {
     using Word = CellT;
@@ -101,16 +83,6 @@ struct LocatorT {
 };
 using Locator = LocatorT<uint64_t>;
 
-// Where the LDS-resident locator lives inside the dynamic LDS of the persistent kernel, and
-// where its source copy lives in global memory (all byte offsets are multiples of 16).
-struct LdsLocatorDesc {
-    const char *src;         // global image, copied verbatim into LDS at kernel start
-    int bytes;               // image size
-    int off_cells, off_verts, off_poly, off_row_off, off_row_edges;
-    double x0, y0, inv_h;
-    int ncx, ncy;
-};
-
 struct TraceArgs {
     const float *x, *y, *m, *n, *l, *te, *tm, *dph;
     uint32_t *rng;
@@ -120,12 +92,10 @@ struct TraceArgs {
     int64_t n_rays, gid_offset;
     const double *tiles;
     Locator loc;
-    LdsLocatorDesc lds;
     int tile_d, nfc, noc, nx, ny, nl;
     double n_g, inv_n_g;
     double threshold;   // ener * efficiency > threshold guard of R2..R5: 0 full colour, 1e-15 single lambda
-    const int32_t *order;   // persistent variants: issue order of the 64-ray chunks (NULL: ascending)
-    int max_hops;   // miss hops a lane may take per pass of the persistent loop (0: unbounded)
+    const int32_t *order;   // Jones-vector variants: issue order of the 64-ray chunks (NULL: ascending)
     const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
     int jtile_d;
     // Jones-vector variants: out-couplings appended as (position, ray index) and binned into
@@ -136,7 +106,7 @@ struct TraceArgs {
     double cert_tol;   // Jones-vector variants: base of the decision certification bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
-    // fused launches (variants 7-9, n_iter > 1): n_iter chained traces of every ray in one
+    // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;
     uint64_t *rng64;
@@ -165,51 +135,6 @@ constexpr int kPolyEff2 = 1;
 constexpr int kPolyIC = 2;
 constexpr int kPolyFC0 = 3;
 
-#if defined(WGRT_DIAG) || defined(WGRT_TIMERS)
-// Diagnostic builds only.  Per-phase shader-clock cycles summed over lanes (grid kernel,
-// WGRT_TIMERS, tools/diag_timers.py): 0 interact: tile + sincos + branch fields, 1 decision,
-// 2 take / eyebox, 3 advance, 4 #interactions, 5 #advance calls.
-__device__ unsigned long long g_diag_tm[8];
-#endif
-#ifdef WGRT_PHASES
-// Diagnostic build only (tools/phases.py): shader cycles per persistent-loop phase, summed
-// over waves: [0] advance, [1] refill, [2] interact, [3] passes, [4..7] the same after the work
-// queue ran dry; [8] per-wave start, [9] exhausted, [10] end (s_memrealtime, summed).
-__device__ unsigned long long g_phase[16];
-
-constexpr int kPhaseWaves = 16384;
-__device__ unsigned long long g_phase_wave_t[kPhaseWaves * 3];
-#endif
-#ifdef WGRT_DIAG
-// Diagnostic build only (tools/diag.py): wave-loop occupancy counters.
-__device__ unsigned long long g_diag[16];
-__device__ unsigned long long g_diag_fallback;
-
-// per-wave timeline (s_memrealtime, 100 MHz): start, queue exhausted, end
-constexpr int kDiagWaves = 16384;
-__device__ unsigned long long g_diag_wave_t[kDiagWaves * 3];
-// region r: g_diag[6 + r] += number of wave executions, g_diag_act[r] += active lanes
-__device__ unsigned long long g_diag_act[16];
-__device__ __forceinline__ void diag_region(int r) {
-    const uint64_t m = __ballot(1);
-    if ((threadIdx.x & 63) == __builtin_ctzll(m)) {
-        atomicAdd(&g_diag[6 + r], 1ull);
-        atomicAdd(&g_diag_act[r], (unsigned long long)__popcll(m));
-    }
-}
-#ifdef WGRT_DIAG_LIGHT
-#define DIAG_REGION(r) ((void)0)   // lane-state counters only: no per-region atomics distorting the timing
-#else
-#define DIAG_REGION(r) diag_region(r)
-#endif
-#else
-#define DIAG_REGION(r) ((void)0)
-#endif
-#ifdef WGRT_ASM_MARKS
-#define ASM_MARK(t) asm volatile(";#MARK " t)
-#else
-#define ASM_MARK(t) ((void)0)
-#endif
 
 // A point's cell of the locator grid: the per-polygon class word and the cell row.
 struct Cell {
@@ -233,7 +158,6 @@ template <class Loc>
 __device__ __forceinline__ bool in_poly(const Loc &L, const Cell &c, int k, double x, double y) {
     const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
-    DIAG_REGION(4);   // exact EDGE-cell test
     const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
     const int r = k * L.ncy + c.cy;
     const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
@@ -276,10 +200,6 @@ template <bool KARG = false, class Loc>
 __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y) {
     const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
-#ifdef WGRT_ABL_EDGE
-    return false;   // ablation build only: EDGE cells count as outside
-#endif
-    DIAG_REGION(4);
     const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
     const int r = k * L.ncy + cy;
     // one 128-B record: the (at most kBandSegs) edges of polygon k meeting this cell row,
@@ -400,37 +320,19 @@ struct Lane {
     int l, m, n;
     uint32_t bounces;  // 1 in-coupling event + loop iterations (GRTF:905)
     bool hit;          // accumulated into matrix_EB
-#ifdef WGRT_TIMERS
-    uint64_t tm[6];
-#endif
 };
-#ifdef WGRT_TIMERS
-#define DIAG_CLK(v) const uint64_t v = __builtin_readcyclecounter()
-#define DIAG_ACC(k, a, b) (L.tm[k] += (b) - (a))
-#else
-#define DIAG_CLK(v) ((void)0)
-#define DIAG_ACC(k, a, b) ((void)0)
-#endif
 
 // Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
 // FoV / wavelength indices fall outside the scene.
 __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L) {
-#ifdef WGRT_ABL_RAYLOAD
-    const int64_t ld = (i & 63) | (i & ~(int64_t)1023);   // ablation build only: 64 cache-hot rays per block
-#else
     const int64_t ld = i;
-#endif
     const int m = (int)A.m[ld], n = (int)A.n[ld], l = A.l ? (int)A.l[ld] : 0;
     if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
     L.i = i;
     L.l = l;
     L.m = m;
     L.n = n;
-#ifdef WGRT_ABL_TILE
-    L.T = A.tiles;   // ablation build only: every ray reads tile 0 (L1-resident)
-#else
     L.T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
-#endif
     L.r.x = (double)A.x[ld];
     L.r.y = (double)A.y[ld];
     L.r.te = (double)A.te[ld];
@@ -446,14 +348,11 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
     L.r.region = 0;
     L.bounces = 1;
     L.hit = false;
-#ifdef WGRT_TIMERS
-    for (int k = 0; k < 6; ++k) L.tm[k] = 0;
-#endif
     return true;
 }
 
 enum : int { kDie = -1, kTransit = -2 };
-constexpr int kChunk = 64;   // rays per work-queue chunk of the persistent variants
+constexpr int kChunk = 64;   // rays per work-queue chunk of the Jones-vector variants (chunk_order unit)
 
 
 
@@ -468,8 +367,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     Ray &r = L.r;
     const double *T = L.T;
     const double *B = T + kTileHeader + kBlock * blk;
-    DIAG_REGION(0);   // interaction
-    DIAG_CLK(t0);
     double sd, cd;
     cd = r.ph.c;
     sd = r.ph.s;
@@ -497,8 +394,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         q[1] = k == 1 ? v : q[1];
         q[2] = k == 2 ? v : q[2];
     }
-    DIAG_CLK(t1);
-    DIAG_ACC(0, t0, t1);
     // 1 / denom to ~1e-16 relative (estimates only): hardware reciprocal + two Newton steps
     double inv = __builtin_amdgcn_rcp(denom);
     inv = fma(inv, fma(-denom, inv, 1.0), inv);
@@ -534,9 +429,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         else if (three && u <= c2 && pass2) b = 2;
         else return kDie;
     } else {
-#ifdef WGRT_DIAG
-        atomicAdd(&g_diag_fallback, 1ull);
-#endif
         double te[3], tm[3];
 #pragma unroll
         for (int k = 0; k < 3; ++k) {
@@ -561,18 +453,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         else return kDie;
     }
 
-    DIAG_CLK(t2);
-    DIAG_ACC(1, t1, t2);
-#ifdef WGRT_TIMERS
-    L.tm[4] += 1;
-    struct Acc {
-        Lane &L;
-        uint64_t t;
-        __device__ ~Acc() { L.tm[2] += __builtin_readcyclecounter() - t; }
-    } acc_{L, t2};
-#endif
     if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
-        DIAG_REGION(2);
         if (inside_or_on_edge(r.x, r.y, T + kTileEbRect, 4)) {
             const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
             const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
@@ -592,7 +473,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         }
         return kDie;
     }
-    DIAG_REGION(1);   // take a branch
     const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * b);
     const double cte = hypot_cr(f.te_re, f.te_im);
     const double ctm = hypot_cr(f.tm_re, f.tm_im);
@@ -613,7 +493,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
     if (kind == 0) {
-        DIAG_REGION(5);
         const bool in_ic = in_poly(loc, locate(loc, r.x, r.y), kPolyIC, r.x, r.y);
         if (b == 0) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
@@ -637,9 +516,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     const int g = (r.region == 2) ? 0 : 2;
     const double gx = T[kTileGap + g], gy = T[kTileGap + g + 1];
     const Phasor hop{T[kTileHopRot + g], T[kTileHopRot + g + 1]};   // 2 * TIR[g / 2]
-    for (int hops = 0;; ++hops) {
-        if (A.max_hops > 0 && hops >= A.max_hops) return kTransit;
-        DIAG_REGION(3);   // loop iteration in advance
+    for (;;) {
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
         const Cell c = locate(loc, r.x, r.y);
@@ -757,11 +634,7 @@ enum : int { kUncertain = -3, kOut = -4 };
 // rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
 __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
                                           uint64_t *gword = nullptr) {
-#ifdef WGRT_ABL_RAYLOAD
-    const int64_t ld = (i & 63) | (i & ~(int64_t)1023);   // ablation build only: 64 cache-hot rays per block
-#else
     const int64_t ld = i;
-#endif
     const float *const cl = KA(l);
     const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
     const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
@@ -770,11 +643,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     const int m = (int)fm, n = (int)fn, l = (int)fl;
     const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
     L.i = i;
-#ifdef WGRT_ABL_TILE
-    L.T = A.jtiles;   // ablation build only: every ray reads tile 0
-#else
     L.T = KA(jtiles) + (ok ? (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d : 0);
-#endif
     L.r.x = (double)fx;
     L.r.y = (double)fy;
     const double te = (double)fte, tm = (double)ftm;
@@ -859,8 +728,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     JRay &r = L.r;
     const double *T = L.T;
     const double *B = T + kJHeader + kJBlock * blk;
-    DIAG_REGION(0);
-    ASM_MARK("interact-begin");
     const bool three = kind >= 3;
     const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
     // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
@@ -878,7 +745,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double xb = r.x + mvb.x, yb = r.y + mvb.y;
     const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
 
-    ASM_MARK("interact-hoploop");
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     for (uint32_t h = 0; h < r.hops; ++h) {
         const double mr = r.mr;
@@ -886,7 +752,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
         r.mi = fma(mr, hop.y, r.mi * hop.x);
     }
     r.hops = 0;
-    ASM_MARK("interact-math");
     const double denom = entry ? cg.x : r.cos_t;
     const double u = rng_draw(r.s, A.gid_offset + L.i);
     const JField f0 = jones(k0, r), f1 = jones(k1, r);
@@ -926,7 +791,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
                  (!three || u > c2 || fabs(g2 - t) > m2);
         }
     }
-    ASM_MARK("interact-decide");
     const bool s0 = (u <= c0) & p0;
     const bool s1 = !s0 & (u <= c1) & p1;
     const bool s2 = !s0 & !s1 & three & (u <= c2) & p2;   // out-coupling (GRTF:1162-1171, 1231-1240)
@@ -939,8 +803,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const int code = !ok ? kUncertain : s2 ? kOut : !(s0 | s1) ? kDie : 0;
     if (code != 0) return code;
     const int b = ba ? 0 : 1;
-    DIAG_REGION(1);
-    ASM_MARK("interact-take");
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double rn = rsq_nr(n2);
     r.er = f.er * rn;
@@ -956,9 +818,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.gx = ba ? mva.x : mvb.x;
     r.gy = ba ? mva.y : mvb.y;
     L.pf = ba ? pa : pb;
-    ASM_MARK("interact-take-end");
     if (kind == 0) {
-        DIAG_REGION(5);
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
@@ -976,10 +836,8 @@ constexpr int kJMaxHops = 1;
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     JRay &r = L.r;
-    ASM_MARK("advance");
     for (int hops = 0;; ++hops) {
         if (hops >= kJMaxHops) return kTransit;
-        DIAG_REGION(3);
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
         const auto c = (typename Loc::Word)L.pf;
@@ -1010,15 +868,8 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
     }
 }
 
-__device__ __forceinline__ uint32_t lane_hit(const Lane &L) { return L.hit; }
-__device__ __forceinline__ uint32_t lane_hit(const JLane &) { return 0; }   // counted by the epilogue
-
 template <class LaneT>
 __device__ __forceinline__ void lane_retire(const TraceArgs &A, const LaneT &L) {
-#ifdef WGRT_ABL_NOSTORE
-    if (L.r.s == 0x12345u && L.bounces == 77777u) A.rng[L.i] = 0;   // ablation build only: (almost) no stores
-    return;
-#endif
     A.rng[L.i] = L.r.s;
     if (A.per_ray) A.per_ray[L.i] = L.bounces;
 }
@@ -1059,24 +910,13 @@ __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_
         if (next < 0) break;
         L.r.region = next;
         entry = false;
-        DIAG_CLK(ta);
-        do {
-            blk = advance(A, A.loc, L, kind);
-        } while (blk == kTransit);
-        DIAG_CLK(tb);
-        DIAG_ACC(3, ta, tb);
-#ifdef WGRT_TIMERS
-        L.tm[5] += 1;
-#endif
+        blk = advance(A, A.loc, L, kind);
         if (blk < 0) break;
     }
     if (s_io) *s_io = L.r.s;
     else lane_retire(A, L);
     b += L.bounces;
     h += L.hit;
-#ifdef WGRT_TIMERS
-    for (int k = 0; k < 6; ++k) atomicAdd(&g_diag_tm[k], (unsigned long long)L.tm[k]);
-#endif
 }
 
 // Variant 1: one ray per lane over a 1-D grid (the reference's launch shape, MAIN:167).
@@ -1130,15 +970,6 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
         atomicAdd((unsigned long long *)&A.stats->replayed, nr);
 }
 
-// Variant 2: persistent waves with lane refill ("wavefront compaction" of terminated
-// rays).  Ray lifetimes are heavy-tailed (most rays die at the in-coupler, a few bounce
-// for tens of iterations), so a wave that owns 64 fixed rays idles most lanes for most of
-// its life.  Each pass of the wave loop (1) runs every live lane through its non-interacting
-// hops up to its next coupler interaction, (2) hands lanes without a ray the next rays of
-// the wave's chunk (ballot + prefix count, no memory traffic), grabbing a new chunk of
-// `chunk` consecutive rays from the global counter when the chunk runs dry, and (3) runs
-// the fp64 interaction math for all lanes together.  Results are identical to variant 1:
-// each ray's evolution depends only on its own state and its global index.
 // Work queue of the Jones-vector variants: one head per XCD (each on its own 128-B line), head
 // x handing out chunks [x n / 8, (x + 1) n / 8) in order, so a die's waves share one stretch
 // of consecutive chunks (FoV x wavelength tiles stay in that XCD's L2) and the dequeue
@@ -1147,245 +978,19 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
 constexpr int kScratchCtr = (kHeads + 2) * kHeadStride;   // heads, replay count, out-coupling slots
-constexpr int kQBlock = 512;   // out-coupling queue slots a wave reserves at a time
+constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
+                               // out-couples ~10 rays per trace; unused slots cost the eyebox
+                               // epilogue a read each)
+// Passes a fused-launch lane may wait for its ray's previous trace before it gives the ray up
+// (counted in wgrt_trace_stats.bad_rays).  A legitimate wait is bounded by that trace's length
+// (<= 1e5 + 1 bounces, at least one per pass of the wave running it); the bound only turns a
+// hand-off bug (epoch / tag) into a visible count instead of a hung GPU.
+constexpr uint32_t kMaxWaitPasses = 1u << 24;
 
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
     return (int)(v & 7u);
-}
-
-// Next chunk for the calling wave (wave-uniform), or -1 when every head is exhausted.
-__device__ __forceinline__ int64_t pop_chunk_xcd(unsigned long long *heads, int &h, int64_t n_chunks, int lane) {
-    for (int tries = 0; tries < kHeads; ++tries) {
-        const int x = (h + tries) & (kHeads - 1);
-        const int64_t lo = n_chunks * x / kHeads, hi = n_chunks * (x + 1) / kHeads;
-        unsigned long long q = 0;
-        if (lane == 0) q = atomicAdd(heads + kHeadStride * x, 1ull);
-        q = __shfl(q, 0);
-        if (lo + (int64_t)q < hi) {
-            h = x;
-            return lo + (int64_t)q;
-        }
-    }
-    return -1;
-}
-
-template <class LaneT, class Loc>
-__device__ __forceinline__ void persistent_body(const TraceArgs &A0, const Loc &loc0, unsigned long long *counter,
-                                                int chunk, bool xcd_heads = false) {
-    const TraceArgs &A = A0;
-    const Loc &loc = loc0;
-    const int lane = threadIdx.x & 63;
-    int head = xcd_heads ? xcc_id() : 0;
-    int pend_h = -1;                  // head of the dequeue in flight (-1: none)
-    unsigned long long pend_v = 0;    // its result (lane 0)
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
-    int64_t cur = 0, end = 0;  // wave-uniform chunk cursor
-    bool exhausted = false;
-    bool active = false;
-    LaneT L;
-    int blk = 0, kind = 0;
-    bool entry = false;
-    uint32_t tot_b = 0, tot_h = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
-#ifdef WGRT_ABL_STATIC
-    int d_static_k = 0;
-#endif
-#ifdef WGRT_DIAG
-    uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_hopmax = 0;
-    const int d_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef WGRT_PHASES
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#ifdef WGRT_PHASES_DRAIN
-    uint64_t ph_drain[2] = {0, 0};
-#endif
-    const int p_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-    for (;;) {
-#ifdef WGRT_PHASES
-        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-        const int pofs = exhausted ? 4 : 0;
-#ifdef WGRT_PHASES_DRAIN
-        // diagnostic: drain everything the previous pass left in flight, timed on its own
-        __builtin_amdgcn_s_waitcnt(0);
-        ph_drain[exhausted ? 1 : 0] += __builtin_amdgcn_s_memtime() - pt0;
-#endif
-#endif
-        if (active) {
-#ifdef WGRT_DIAG
-            const uint32_t b0 = L.bounces;
-#endif
-            blk = advance(A, loc, L, kind);
-#ifdef WGRT_DIAG
-            uint32_t hops = L.bounces - b0 - (blk >= 0 ? 1u : 0u);
-            d_hops += hops;
-            for (int o = 32; o > 0; o >>= 1) hops = max(hops, (uint32_t)__shfl_xor((int)hops, o));
-            d_hopmax += hops;
-#endif
-            entry = false;
-            if (blk == kDie) {
-                lane_retire(A, L);
-                tot_b += L.bounces;
-                tot_h += lane_hit(L);
-                active = false;
-            }
-        }
-#ifdef WGRT_PHASES
-        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
-#endif
-        uint64_t need = __ballot(!active);
-        while (need != 0ull && !exhausted) {
-            if (cur >= end) {
-                unsigned long long q = 0;
-#ifdef WGRT_ABL_STATIC
-                // ablation build only: wave w takes chunks w, w + W, w + 2W, ... (no atomics)
-                {
-                    const unsigned long long W = (unsigned long long)gridDim.x * (blockDim.x >> 6);
-                    const unsigned long long w = (unsigned long long)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-                    q = w + W * (unsigned long long)(d_static_k++);
-                }
-#else
-                const int64_t n_chunks_ = (A.n_rays + chunk - 1) / chunk;
-                if (xcd_heads) {
-                    // the dequeue for this chunk was issued when the previous one started
-                    // (pend_v, on head pend_h): its latency overlapped that chunk's passes
-                    int64_t c = -1;
-                    if (pend_h >= 0) {
-                        const unsigned long long pq = __shfl(pend_v, 0);
-                        const int64_t lo = n_chunks_ * pend_h / kHeads, hi = n_chunks_ * (pend_h + 1) / kHeads;
-                        if (lo + (int64_t)pq < hi) c = lo + (int64_t)pq;
-                        else head = (pend_h + 1) & (kHeads - 1);   // that head ran dry: move on
-                    }
-                    if (c < 0) c = pop_chunk_xcd(counter, head, n_chunks_, lane);
-                    q = c < 0 ? (unsigned long long)n_chunks_ : (unsigned long long)c;
-                    pend_h = -1;
-                    if (c >= 0) {   // issue the next dequeue now; it is read when this chunk runs dry
-                        pend_h = head;
-                        if (lane == 0) pend_v = atomicAdd(counter + kHeadStride * head, 1ull);
-                    }
-                } else {
-                    if (lane == 0) q = atomicAdd(counter, 1ull);
-                    q = __shfl(q, 0);
-                }
-#endif
-                const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
-                if ((int64_t)q >= n_chunks) {
-                    exhausted = true;
-#ifdef WGRT_PHASES
-                    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef WGRT_DIAG
-                    {
-                        const int wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-                        if (lane == 0 && wid < kDiagWaves) g_diag_wave_t[3 * wid + 1] = __builtin_amdgcn_s_memrealtime();
-                    }
-#endif
-                    break;
-                }
-                cur = (int64_t)(A.order ? A.order[q] : (int64_t)q) * chunk;
-                end = cur + chunk < A.n_rays ? cur + chunk : A.n_rays;
-            }
-            const int want = __popcll(need);
-            const int64_t avail = end - cur;
-            const int take = (int64_t)want < avail ? want : (int)avail;
-            if (!active) {
-                const int rank = __popcll(need & lt_mask);
-                if (rank < take) {
-                    DIAG_REGION(6);
-                    if (lane_load(A, cur + rank, L)) {
-                        active = true;
-                        blk = 0;
-                        kind = 0;
-                        entry = true;
-                    } else {
-                        ++tot_bad;
-                    }
-                }
-            }
-            cur += take;
-            need = __ballot(!active);
-        }
-        if (__ballot(active) == 0ull) break;  // queue exhausted and no ray in flight
-#ifdef WGRT_PHASES
-        const uint64_t pt2 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef WGRT_DIAG
-        {
-            const uint64_t na = __popcll(__ballot(active));
-            d_pass += 1;
-            d_act += na;
-            if (exhausted) {
-                d_pass_x += 1;
-                d_act_x += na;
-            }
-        }
-#endif
-        if (active && blk >= 0) {
-            const int next = interact(A, loc, L, blk, kind, entry);
-            if (next == kUncertain) {
-                // abandoned without side effects (Jones-vector variants): replay_kernel re-traces it
-                A.replay_list[atomicAdd(A.replay_count, 1ull)] = (uint32_t)L.i;
-                active = false;
-            } else if (next < 0) {
-                lane_retire(A, L);
-                tot_b += L.bounces;
-                tot_h += lane_hit(L);
-                active = false;
-            } else {
-                L.r.region = next;
-            }
-        }
-#ifdef WGRT_PHASES
-        {
-            const uint64_t pt3 = __builtin_amdgcn_s_memtime();
-            ph[pofs + 0] += pt1 - pt0;
-            ph[pofs + 1] += pt2 - pt1;
-            ph[pofs + 2] += pt3 - pt2;
-            ph[pofs + 3] += 1;
-        }
-#endif
-    }
-#ifdef WGRT_PHASES
-    if (lane == 0) {
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
-#ifdef WGRT_PHASES_DRAIN
-        atomicAdd(&g_phase[11], (unsigned long long)ph_drain[0]);
-        atomicAdd(&g_phase[12], (unsigned long long)ph_drain[1]);
-#endif
-        if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-    add_stats(A0.stats, tot_b, tot_h, tot_bad);
-#ifdef WGRT_DIAG
-    if (lane == 0) {
-        if (d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 2] = __builtin_amdgcn_s_memrealtime();
-        atomicAdd(&g_diag[0], d_pass);
-        atomicAdd(&g_diag[1], d_act);
-        atomicAdd(&g_diag[2], d_pass_x);
-        atomicAdd(&g_diag[3], d_act_x);
-        atomicAdd(&g_diag[5], d_hopmax);
-    }
-    d_hops = wave_sum(d_hops);
-    if (lane == 0) atomicAdd(&g_diag[4], d_hops);
-#endif
-}
-
-// Variant 2: the persistent loop with the locator read from global memory (L2-resident).
-__global__ __launch_bounds__(256, 3) void trace_persistent_kernel(TraceArgs A, unsigned long long *counter,
-                                                                  int chunk) {
-    persistent_body<Lane>(A, A.loc, counter, chunk);
-}
-
-// Variants 4-6: variant 2 at W waves per SIMD (W = 4: register budget 128)
-// and/or with 32-bit cell words in global memory (scenes of <= 16 polygons: half the
-// grid's cache footprint).
-template <class CellT, int W>
-__global__ __launch_bounds__(256, W) void trace_persistent_g_kernel(TraceArgs A, LocatorT<CellT> loc,
-                                                                    unsigned long long *counter, int chunk) {
-    persistent_body<Lane>(A, loc, counter, chunk);
 }
 
 // Tag of a fused launch's per-ray RNG word: launch epoch, broken flag, traces completed.
@@ -1419,20 +1024,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
-    uint32_t tot_b = 0, tot_bad = 0;   // per lane: < 2^32 for any launch that fits in memory
+    uint64_t tot_b = 0, tot_bad = 0;   // per lane, over every trace the lane runs
+    uint32_t wait_passes = 0;          // fused: passes spent waiting for the current ray
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
-#ifdef WGRT_PHASES
-    uint64_t ph[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-    const int p_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef WGRT_DIAG
-    uint64_t d_pass = 0, d_act = 0, d_pass_x = 0, d_act_x = 0, d_hops = 0, d_wait = 0;
-    uint64_t d_free_b = 0, d_transit_b = 0, d_wait_b = 0;   // lane states per pass before the queue ran dry
-    const int d_wid = blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid] = __builtin_amdgcn_s_memrealtime();
-#endif
 
     // head x's items: iteration-major over its chunk range [lo, hi)
     auto decode = [&](int x, int64_t q, int64_t &c, uint32_t &k) -> bool {
@@ -1461,6 +1056,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 return;   // abandoned in an earlier iteration: the replay kernel finishes it
             } else {
                 waiting = true;
+                wait_passes = 0;
                 return;
             }
         }
@@ -1484,20 +1080,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     };
 
     for (;;) {
-#ifdef WGRT_PHASES
-        const uint64_t pt0 = __builtin_amdgcn_s_memtime();
-        const int pofs = exhausted ? 4 : 0;
-#endif
-        ASM_MARK("pass-top");
         if (active) {
             blk = advance(A, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
-#ifdef WGRT_PHASES
-        const uint64_t pt1 = __builtin_amdgcn_s_memtime();
-#endif
-        ASM_MARK("refill");
         if (FUSED && waiting) {
             // poll only the previous trace's granule: the ray's columns are still in L from the
             // start() that found it not ready
@@ -1513,6 +1100,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 entry = true;
             } else if ((tag >> 8) == ((A.iter_epoch << 1) | 1u)) {
                 waiting = false;   // abandoned in an earlier iteration: the replay kernel finishes it
+            } else if (++wait_passes > kMaxWaitPasses) {
+                waiting = false;   // hand-off never arrived: give the ray up, visibly
+                ++tot_bad;
             }
         }
         uint64_t need = __ballot(!active && !waiting);
@@ -1541,12 +1131,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 pend_h = -1;
                 if (!got) {
                     exhausted = true;
-#ifdef WGRT_PHASES
-                    if (lane == 0 && p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
-#ifdef WGRT_DIAG
-                    if (lane == 0 && d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 1] = __builtin_amdgcn_s_memrealtime();
-#endif
                     break;
                 }
                 pend_h = head;   // issue the next dequeue now; read when this item runs dry
@@ -1573,28 +1157,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             need = __ballot(!active && !waiting);
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
-        ASM_MARK("pre-interact");
         bool out = false;
-#ifdef WGRT_PHASES
-        const uint64_t pt2 = __builtin_amdgcn_s_memtime();
-#endif
-#ifdef WGRT_DIAG
-        {
-            const uint64_t na = __popcll(__ballot(active && blk >= 0));
-            d_pass += 1;
-            d_act += na;
-            d_wait += __popcll(__ballot(waiting));
-            if (exhausted) {
-                d_pass_x += 1;
-                d_act_x += na;
-            } else {
-                d_free_b += __popcll(__ballot(!active && !waiting));
-                d_transit_b += __popcll(__ballot(active && blk < 0));
-                d_wait_b += __popcll(__ballot(waiting));
-            }
-            d_hops += (active && blk == kTransit) ? 1 : 0;
-        }
-#endif
         if (active && blk >= 0) {
             const int next = interact(A, loc, L, blk, kind, entry);
             if (next == kOut) {
@@ -1614,7 +1177,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 L.r.region = next;
             }
         }
-        ASM_MARK("post-interact");
         // out-couplings of this pass go to the wave's block of queue slots (a contended returning
         // atomic per pass would put its latency on every pass; a new block is needed about
         // once per hundred passes)
@@ -1638,76 +1200,18 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 qfill += nout;
             }
         }
-#ifdef WGRT_PHASES
-        {
-            const uint64_t pt3 = __builtin_amdgcn_s_memtime();
-            ph[pofs + 0] += pt1 - pt0;
-            ph[pofs + 1] += pt2 - pt1;
-            ph[pofs + 2] += pt3 - pt2;
-            ph[pofs + 3] += 1;
-        }
-#endif
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
     add_stats(KA(stats), tot_b, 0, tot_bad);
-#ifdef WGRT_PHASES
-    if (lane == 0) {
-        for (int k = 0; k < 8; ++k) atomicAdd(&g_phase[k], (unsigned long long)ph[k]);
-        if (p_wid < kPhaseWaves) g_phase_wave_t[3 * p_wid + 2] = __builtin_amdgcn_s_memrealtime();
-    }
-#endif
-#ifdef WGRT_DIAG
-    if (lane == 0) {
-        if (d_wid < kDiagWaves) g_diag_wave_t[3 * d_wid + 2] = __builtin_amdgcn_s_memrealtime();
-        atomicAdd(&g_diag[0], d_pass);
-        atomicAdd(&g_diag[1], d_act);
-        atomicAdd(&g_diag[2], d_pass_x);
-        atomicAdd(&g_diag[3], d_act_x);
-        atomicAdd(&g_diag[5], d_wait);
-        atomicAdd(&g_diag[13], d_free_b);
-        atomicAdd(&g_diag[14], d_transit_b);
-        atomicAdd(&g_diag[15], d_wait_b);
-    }
-    d_hops = wave_sum(d_hops);
-    if (lane == 0) atomicAdd(&g_diag[4], d_hops);
-#endif
 }
 
-// Variants 7-9: the persistent loop over the Jones-vector path (32-bit cell words at W waves
-// per SIMD; 64-bit cell words for scenes of more than 16 polygons).
-template <class CellT, int W, bool FUSED = false>
-__global__ __launch_bounds__(256, W) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
+// Variants 7 / 9: the persistent loop over the Jones-vector path, 3 waves per SIMD (32-bit cell
+// words; 64-bit cell words for scenes of more than 16 polygons).
+constexpr int kJonesWaves = 3;
+template <class CellT, bool FUSED>
+__global__ __launch_bounds__(256, kJonesWaves) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
     jones_body<FUSED>(A, loc, counter, chunk);
-}
-
-// Variant 3: the persistent loop with the whole locator (cell classes, polygon vertices,
-// row-band edge lists) staged once into LDS by every workgroup, so the per-hop membership
-// tests cost LDS reads instead of dependent L2 round trips.  One 768-thread workgroup
-// (12 waves, 3 per SIMD) per CU shares one LDS copy of up to ~150 KB.
-__global__ __launch_bounds__(768, 1) void trace_persistent_lds_kernel(TraceArgs A, unsigned long long *counter,
-                                                                      int chunk) {
-    extern __shared__ __attribute__((aligned(16))) char smem[];
-    const LdsLocatorDesc &D = A.lds;
-    {
-        const uint4 *src = (const uint4 *)D.src;
-        uint4 *dst = (uint4 *)smem;
-        for (int k = threadIdx.x; k < D.bytes / 16; k += blockDim.x) dst[k] = src[k];
-    }
-    __syncthreads();
-    LocatorT<uint32_t> loc;
-    loc.cells = (const uint32_t *)(smem + D.off_cells);
-    loc.verts = (const double *)(smem + D.off_verts);
-    loc.poly_off = (const int32_t *)(smem + D.off_poly);
-    loc.row_off = (const int32_t *)(smem + D.off_row_off);
-    loc.row_edges = (const int32_t *)(smem + D.off_row_edges);
-    loc.bands = nullptr;
-    loc.x0 = D.x0;
-    loc.y0 = D.y0;
-    loc.inv_h = D.inv_h;
-    loc.ncx = D.ncx;
-    loc.ncy = D.ncy;
-    persistent_body<Lane>(A, loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -1719,8 +1223,8 @@ __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, con
     const uint64_t ww = locate_w(L, x, y);
     uint64_t mask = 0, mism = 0;
     for (int k = 0; k < npoly; ++k) {
-        const bool a = in_poly(L, w, k, x, y);      // CSR row lists (variants 1-6)
-        const bool b = in_poly_w(L, ww, k, x, y);   // 128-B band records (variants 7-9)
+        const bool a = in_poly(L, w, k, x, y);      // CSR row lists (exact lane)
+        const bool b = in_poly_w(L, ww, k, x, y);   // 128-B band records (Jones-vector lane)
         if (a) mask |= 1ull << k;
         if (a != b) mism = 1ull << 63;
     }
@@ -1801,24 +1305,12 @@ struct wgrt_scene {
     double *d_bands = nullptr;
     LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
     int64_t tiles = 0;
-    // work counters of the persistent kernel: a ring, so launches in flight on different
-    // streams never share one (each launch zeroes its slot with hipMemsetAsync first)
-    static constexpr int kCounterSlots = 64;
-    unsigned long long *d_counters = nullptr;
-    std::atomic<unsigned> next_counter{0};
-    int persistent_grid = 0;   // resident 256-thread workgroups of variant 2
-    int persistent_w2_grid = 0;   // ... of variant 4
-    int lds_grid = 0;          // resident 768-thread workgroups of variant 3 (0: unavailable)
-    char *d_lds_image = nullptr;
-    size_t lds_bytes = 0;
-    LdsImage lds;              // offsets / grid parameters (bytes released after upload)
     int jones_grid = 0;        // resident 256-thread workgroups of variant 7
-    int jones_w4_grid = 0;     // ... of variant 8
     int jones64_grid = 0;      // ... of variant 9
-    // Jones-vector launches: per-stream work counter + replay list (launches on one stream are
-    // ordered, so they may share; launches on different streams never do)
+    // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so
+    // they may share it; launches on different streams never do)
     struct Scratch {
-        unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), then the replay count
+        unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), replay count, queue count
         uint32_t *list = nullptr;            // replay list
         int64_t cap = 0;                     // replay list entries
         double2 *q_xy = nullptr;             // out-coupling queue: position, ray index
@@ -1847,6 +1339,19 @@ Locator make_locator(const wgrt_scene *s) {
     L.inv_h = s->loc_host.inv_h;
     L.ncx = s->loc_host.ncx;
     L.ncy = s->loc_host.ncy;
+    return L;
+}
+
+LocatorT<uint32_t> make_locator32(const wgrt_scene *s) {
+    const Locator g = make_locator(s);
+    LocatorT<uint32_t> L;
+    L.cells = s->d_cells32;
+    L.verts = g.verts;
+    L.poly_off = g.poly_off;
+    L.row_off = g.row_off;
+    L.row_edges = g.row_edges;
+    L.bands = g.bands;
+    L.x0 = g.x0, L.y0 = g.y0, L.inv_h = g.inv_h, L.ncx = g.ncx, L.ncy = g.ncy;
     return L;
 }
 
@@ -1905,48 +1410,12 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         }
     }
     {
-        hipError_t e = hipMalloc((void **)&s->d_counters, sizeof(unsigned long long) * wgrt_scene::kCounterSlots);
-        if (e != hipSuccess) {
-            wgrt_scene_destroy(s);
-            return fail(WGRT_ERR_HIP, std::string("hipMalloc(counters): ") + hipGetErrorString(e));
-        }
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_kernel, 256, 0));
-        s->persistent_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_persistent_g_kernel<uint64_t, 4>, 256, 0));
-        s->persistent_w2_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, 3>, 256, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, false>, 256, 0));
         s->jones_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, WGRT_W8>, 256, 0));
-        s->jones_w4_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint64_t, 3>, 256, 0));
+        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint64_t, false>, 256, 0));
         s->jones64_grid = std::max(1, cus * std::max(1, per_cu));
-        if (host.lds.ok) {
-            const int bytes = (int)host.lds.bytes.size();
-            int lds_max = 0;
-            HIP_TRY(hipDeviceGetAttribute(&lds_max, hipDeviceAttributeMaxSharedMemoryPerBlock, device));
-            if (bytes <= lds_max) {
-                (void)hipFuncSetAttribute((const void *)trace_persistent_lds_kernel,
-                                          hipFuncAttributeMaxDynamicSharedMemorySize, bytes);
-                int per_cu_lds = 0;
-                HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu_lds, trace_persistent_lds_kernel,
-                                                                     768, bytes));
-                if (per_cu_lds > 0) {
-                    wgrt_status st2 = upload(host.lds.bytes, &s->d_lds_image);
-                    if (st2 != WGRT_OK) {
-                        wgrt_scene_destroy(s);
-                        return st2;
-                    }
-                    s->lds_grid = cus * per_cu_lds;
-                }
-            }
-        }
-        s->lds_bytes = host.lds.bytes.size();
-        s->lds = host.lds;
-        s->lds.bytes.clear();
-        s->lds.bytes.shrink_to_fit();
-        s->lds.ok = s->lds_grid > 0;
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
@@ -1968,11 +1437,9 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_cells32);
     (void)hipFree(s->d_verts);
     (void)hipFree(s->d_poly_off);
-    (void)hipFree(s->d_counters);
     (void)hipFree(s->d_row_off);
     (void)hipFree(s->d_row_edges);
     (void)hipFree(s->d_bands);
-    (void)hipFree(s->d_lds_image);
     for (auto &kv : s->scratch) {
         (void)hipFree(kv.second.ctr);
         (void)hipFree(kv.second.list);
@@ -1993,17 +1460,22 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->grid_cell_mm = s->loc_host.h;
     info->grid_edge_cells = s->loc_host.edge_cells;
     info->n_polygons = s->npoly;
-    info->lds_locator_bytes = s->lds_grid > 0 ? (int64_t)s->lds_bytes : 0;
-    info->lds_cell_mm = s->lds_grid > 0 ? s->lds.h : 0.0;
     info->device = s->device;
+    info->jtile_bytes = (int64_t)s->jtile_d * 8;
     return WGRT_OK;
 }
 
+}  // extern "C"
+
+namespace {
+
 // The Jones-vector variants' per-stream launch scratch (work-queue heads, replay list,
 // out-coupling queue, fused-launch granules), grown to n_rays x num_iter traces on `grid`
-// workgroups.  Growing synchronises the stream (the old buffers may be in use).
-static wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num_iter, int64_t grid,
-                                  wgrt_scene::Scratch **out) {
+// workgroups.  Growing synchronises the stream (the old buffers may be in use).  For a fused
+// launch (epoch != NULL) the launch epoch of the granule tags is advanced here, under the same
+// lock, and returned.
+wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num_iter, int64_t grid,
+                           wgrt_scene::Scratch **out, uint32_t *epoch = nullptr) {
     hipStream_t st = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(ms->scratch_mu);
     wgrt_scene::Scratch *sc = &ms->scratch[stream];
@@ -2050,6 +1522,13 @@ static wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, 
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
         sc->cap64 = n_rays;
     }
+    if (epoch) {
+        if (++sc->iter_epoch >= (1u << 23)) {   // granule tags wrapped: clear them
+            HIP_TRY(hipMemsetAsync(sc->rng64, 0, (size_t)sc->cap64 * sizeof(uint64_t), st));
+            sc->iter_epoch = 1;
+        }
+        *epoch = sc->iter_epoch;
+    }
     return WGRT_OK;
 }
 
@@ -2057,30 +1536,30 @@ static wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, 
 // process_rays_kernel_pro (GRTF:419-831) -- no lmd_num column, wavelength 0 of a
 // one-wavelength scene, threshold 1e-15; otherwise process_rays_kernel_pro_fullColor
 // (GRTF:833-1246), threshold 0.  The two kernels differ in nothing else.
-static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
-                                uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
-                                uint32_t *per_ray_bounces, void *stream, int variant, int workgroups, bool single,
-                                const int32_t *chunk_order = nullptr, int64_t n_chunk_order = 0,
-                                int num_iter = 1) {
+wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                         uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats, uint32_t *per_ray_bounces,
+                         void *stream, int variant, int workgroups, bool single, const int32_t *chunk_order = nullptr,
+                         int64_t n_chunk_order = 0, int num_iter = 1) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
     if (single && s->nl != 1)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "single-wavelength trace needs a scene built with num_lmd == 1");
-    if (n_rays == 0) return WGRT_OK;
-    if (!rays->x || !rays->y || !rays->m || !rays->n || (!single && !rays->lmd_num) || !rays->te || !rays->tm ||
-        !rays->delta_phase || !rng_states || !matrix_EB)
-        return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL ray column / rng_states / matrix_EB");
-    if (variant < 0 || variant > 9) return fail(WGRT_ERR_INVALID_ARGUMENT, "unknown kernel variant");
-    if ((variant == 5 || variant == 6 || variant == 7 || variant == 8) && !s->d_cells32)
-        return fail(WGRT_ERR_UNSUPPORTED, "variants 5-8 need <= 16 polygons");
-    if (variant >= 7 && n_rays > 0xffffffffll)
-        return fail(WGRT_ERR_UNSUPPORTED, "variants 7-9 index at most 2^32 - 1 rays per launch");
-    if (variant == 0) variant = s->d_cells32 ? 7 : (n_rays <= 0xffffffffll ? 9 : 2);   // auto
+    if (variant != 0 && variant != 1 && variant != 7 && variant != 9)
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "kernel variant must be 0 (auto), 1, 7 or 9");
     if (num_iter < 1) num_iter = 1;
     if (num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter must be <= 255");
     if (num_iter > 1 && (per_ray_bounces || chunk_order))
         return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter > 1 takes no per_ray_bounces / chunk_order");
-    if (num_iter > 1 && variant < 7) {   // chained launches, as the reference issues them
+    if (chunk_order && variant == 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order needs variant 0, 7 or 9");
+    if (n_rays == 0) return WGRT_OK;
+    if (!rays->x || !rays->y || !rays->m || !rays->n || (!single && !rays->lmd_num) || !rays->te || !rays->tm ||
+        !rays->delta_phase || !rng_states || !matrix_EB)
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL ray column / rng_states / matrix_EB");
+    if (variant == 7 && !s->d_cells32) return fail(WGRT_ERR_UNSUPPORTED, "variant 7 needs <= 16 polygons");
+    if (variant >= 7 && n_rays > 0xffffffffll)
+        return fail(WGRT_ERR_UNSUPPORTED, "variants 7 / 9 index at most 2^32 - 1 rays per launch");
+    if (variant == 0) variant = n_rays > 0xffffffffll ? 1 : (s->d_cells32 ? 7 : 9);   // auto
+    if (num_iter > 1 && variant == 1) {   // chained launches, as the reference issues them
         for (int it = 0; it < num_iter; ++it) {
             const wgrt_status e = trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, nullptr,
                                                stream, variant, workgroups, single);
@@ -2088,22 +1567,16 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
         }
         return WGRT_OK;
     }
-    TraceArgs A;
+    if (chunk_order && n_chunk_order != (n_rays + kChunk - 1) / kChunk)
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order must list ceil(n_rays / 64) chunks");
+    TraceArgs A{};
     A.x = rays->x;
     A.y = rays->y;
     A.m = rays->m;
     A.n = rays->n;
     A.l = single ? nullptr : rays->lmd_num;
     A.threshold = single ? 1e-15 : 0.0;
-    A.order = nullptr;
-    if (chunk_order) {
-        // a permutation of the 64-ray chunks (validated by the caller: trusted device data)
-        if (n_chunk_order != (n_rays + kChunk - 1) / kChunk)
-            return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order must list ceil(n_rays / 64) chunks");
-        if (variant == 1)
-            return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order needs a persistent variant");
-        A.order = chunk_order;
-    }
+    A.order = chunk_order;   // a permutation of the 64-ray chunks (trusted device data)
     A.te = rays->te;
     A.tm = rays->tm;
     A.dph = rays->delta_phase;
@@ -2115,7 +1588,6 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.gid_offset = gid_offset;
     A.tiles = s->d_tiles;
     A.loc = make_locator(s);
-    A.lds = LdsLocatorDesc{};
     A.tile_d = s->tile_d;
     A.nfc = s->nfc;
     A.noc = s->noc;
@@ -2124,138 +1596,70 @@ static wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int6
     A.nl = s->nl;
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
-    A.max_hops = g_max_hops;
     A.cert_tol = g_cert_tol;
-    A.replay_count = nullptr;
-    A.replay_list = nullptr;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
-    A.q_xy = nullptr;
-    A.q_i = nullptr;
-    A.q_count = nullptr;
     A.n_iter = 1;
-    A.rng64 = nullptr;
-    A.iter_epoch = 0;
     hipStream_t st = (hipStream_t)stream;
-    if (variant >= 7) {
-        int64_t grid = workgroups > 0 ? workgroups
-                                      : (variant == 7 ? s->jones_grid : variant == 8 ? s->jones_w4_grid : s->jones64_grid);
-        const int64_t useful = (n_rays + 255) / 256;
-        if (grid > useful) grid = useful;
-        wgrt_scene *ms = const_cast<wgrt_scene *>(s);
-        wgrt_scene::Scratch *sc = nullptr;
-        {
-            const wgrt_status e = ensure_scratch(ms, stream, n_rays, num_iter, grid, &sc);
-            if (e != WGRT_OK) return e;
-        }
-        if (num_iter > 1) {
-            if (++sc->iter_epoch >= (1u << 23)) {   // granule tags wrapped: clear them
-                HIP_TRY(hipMemsetAsync(sc->rng64, 0, (size_t)sc->cap64 * sizeof(uint64_t), st));
-                sc->iter_epoch = 1;
-            }
-            A.n_iter = num_iter;
-            A.rng64 = sc->rng64;
-            A.iter_epoch = sc->iter_epoch;
-        }
-        A.replay_count = sc->ctr + kHeads * kHeadStride;
-        A.replay_list = sc->list;
-        A.q_xy = sc->q_xy;
-        A.q_i = sc->q_i;
-        A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
-        HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
-        const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
-        A.max_hops = kJMaxHops;   // informational: the Jones loop has it compiled in
-        LocatorT<uint32_t> l32;
-        l32.cells = s->d_cells32;
-        l32.verts = A.loc.verts;
-        l32.poly_off = A.loc.poly_off;
-        l32.row_off = A.loc.row_off;
-        l32.row_edges = A.loc.row_edges;
-        l32.bands = A.loc.bands;
-        l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
-        if (num_iter > 1) {
-            if (variant == 9)
-                hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3, true>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   A.loc, sc->ctr, jchunk);
-            else
-                hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3, true>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   l32, sc->ctr, jchunk);
-        } else if (variant == 7)
-            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
-                               sc->ctr, jchunk);
-        else if (variant == 8)
-            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, WGRT_W8>), dim3((unsigned)grid), dim3(256), 0, st, A, l32,
-                               sc->ctr, jchunk);
-        else
-            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A, A.loc,
-                               sc->ctr, jchunk);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(eyebox_kernel, dim3(1024), dim3(256), 0, st, A);
-        HIP_TRY(hipGetLastError());
-        hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
-    } else if (variant == 1) {
+    if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
         if (blocks > 0x7fffffff) return fail(WGRT_ERR_INVALID_ARGUMENT, "too many rays for one launch");
         hipLaunchKernelGGL(trace_grid_kernel, dim3((unsigned)blocks), dim3(256), 0, st, A);
-    } else {
-        const bool use_lds = variant == 3;
-        if (use_lds && s->lds_grid == 0)
-            return fail(WGRT_ERR_UNSUPPORTED, "variant 3 needs the locator to fit in LDS (<= 16 polygons)");
-        wgrt_scene *ms = const_cast<wgrt_scene *>(s);
-        unsigned long long *ctr = ms->d_counters + (ms->next_counter++ % wgrt_scene::kCounterSlots);
-        HIP_TRY(hipMemsetAsync(ctr, 0, sizeof(unsigned long long), st));
-        const int tpb = use_lds ? 768 : 256;
-        int64_t grid = workgroups > 0 ? workgroups
-                                      : (use_lds ? s->lds_grid
-                                         : (variant == 4 || variant == 6) ? s->persistent_w2_grid
-                                                                          : s->persistent_grid);
-        const int64_t useful = (n_rays + tpb - 1) / tpb;   // never more workgroups than rays / tpb
-        if (grid > useful) grid = useful;
-        if (use_lds) {
-            A.lds.src = s->d_lds_image;
-            A.lds.bytes = (int)s->lds_bytes;
-            A.lds.off_cells = s->lds.off_cells;
-            A.lds.off_verts = s->lds.off_verts;
-            A.lds.off_poly = s->lds.off_poly;
-            A.lds.off_row_off = s->lds.off_row_off;
-            A.lds.off_row_edges = s->lds.off_row_edges;
-            A.lds.x0 = s->lds.x0;
-            A.lds.y0 = s->lds.y0;
-            A.lds.inv_h = s->lds.inv_h;
-            A.lds.ncx = s->lds.ncx;
-            A.lds.ncy = s->lds.ncy;
-            hipLaunchKernelGGL(trace_persistent_lds_kernel, dim3((unsigned)grid), dim3(768), (unsigned)s->lds_bytes,
-                               st, A, ctr, kChunk);
-        } else if (variant >= 4) {
-            LocatorT<uint32_t> l32;
-            l32.cells = s->d_cells32;
-            l32.verts = A.loc.verts;
-            l32.poly_off = A.loc.poly_off;
-            l32.row_off = A.loc.row_off;
-            l32.row_edges = A.loc.row_edges;
-            l32.x0 = A.loc.x0, l32.y0 = A.loc.y0, l32.inv_h = A.loc.inv_h, l32.ncx = A.loc.ncx, l32.ncy = A.loc.ncy;
-            if (variant == 4)
-                hipLaunchKernelGGL((trace_persistent_g_kernel<uint64_t, 4>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   A.loc, ctr, kChunk);
-            else if (variant == 5)
-                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 3>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   l32, ctr, kChunk);
-            else
-                hipLaunchKernelGGL((trace_persistent_g_kernel<uint32_t, 4>), dim3((unsigned)grid), dim3(256), 0, st, A,
-                                   l32, ctr, kChunk);
-        } else {
-            hipLaunchKernelGGL(trace_persistent_kernel, dim3((unsigned)grid), dim3(256), 0, st, A, ctr, kChunk);
-        }
+        HIP_TRY(hipGetLastError());
+        return WGRT_OK;
     }
+    int64_t grid = workgroups > 0 ? workgroups : (variant == 7 ? s->jones_grid : s->jones64_grid);
+    const int64_t useful = (n_rays + 255) / 256;
+    if (grid > useful) grid = useful;
+    wgrt_scene *ms = const_cast<wgrt_scene *>(s);
+    wgrt_scene::Scratch *sc = nullptr;
+    uint32_t epoch = 0;
+    {
+        const wgrt_status e = ensure_scratch(ms, stream, n_rays, num_iter, grid, &sc, num_iter > 1 ? &epoch : nullptr);
+        if (e != WGRT_OK) return e;
+    }
+    if (num_iter > 1) {
+        A.n_iter = num_iter;
+        A.rng64 = sc->rng64;
+        A.iter_epoch = epoch;
+    }
+    A.replay_count = sc->ctr + kHeads * kHeadStride;
+    A.replay_list = sc->list;
+    A.q_xy = sc->q_xy;
+    A.q_i = sc->q_i;
+    A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
+    HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
+    const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
+    const dim3 g3((unsigned)grid), b3(256);
+    if (variant == 9) {
+        if (num_iter > 1)
+            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, true>), g3, b3, 0, st, A, A.loc, sc->ctr, jchunk);
+        else
+            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, false>), g3, b3, 0, st, A, A.loc, sc->ctr, jchunk);
+    } else {
+        const LocatorT<uint32_t> l32 = make_locator32(s);
+        if (num_iter > 1)
+            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, true>), g3, b3, 0, st, A, l32, sc->ctr, jchunk);
+        else
+            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, false>), g3, b3, 0, st, A, l32, sc->ctr, jchunk);
+    }
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(eyebox_kernel, dim3(1024), dim3(256), 0, st, A);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }
+
+}  // namespace
+
+extern "C" {
 
 wgrt_status wgrt_scene_reserve(const wgrt_scene *s, int64_t n_rays, int num_iter, void *stream) {
     if (!s) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene");
     if (n_rays < 0 || num_iter < 0 || num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "bad n_rays / num_iter");
     if (n_rays == 0) return WGRT_OK;
-    const int64_t grid = std::max<int64_t>(std::max<int64_t>(s->jones_grid, s->jones_w4_grid), s->jones64_grid);
+    const int64_t grid = std::max<int64_t>(s->jones_grid, s->jones64_grid);
     wgrt_scene::Scratch *sc = nullptr;
     return ensure_scratch(const_cast<wgrt_scene *>(s), stream, n_rays, std::max(num_iter, 1),
                           std::min<int64_t>(grid, (n_rays + 255) / 256), &sc);
@@ -2351,8 +1755,8 @@ wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, doub
     return WGRT_OK;
 }
 
-wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, int which, const double *xy,
-                                       int64_t n, uint64_t *out_mask) {
+wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, const double *xy, int64_t n,
+                                       uint64_t *out_mask) {
     if (!desc || (n > 0 && (!xy || !out_mask))) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (!(cell_mm > 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be > 0");
     SceneHost host;
@@ -2362,30 +1766,14 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
     const int npoly = (int)host.loc.poly_off.size() - 1;
-    if (which == 1 && !host.lds.ok) return fail(WGRT_ERR_UNSUPPORTED, "no LDS locator image for this scene");
     // host replica of the device locator (same arithmetic as locate / in_poly)
     LocatorT<uint64_t> g{};
-    std::vector<uint64_t> cells64;
-    if (which == 0) {
-        g.cells = host.loc.cells.data();
-        g.verts = host.loc.verts.data();
-        g.poly_off = host.loc.poly_off.data();
-        g.row_off = host.loc.row_off.data();
-        g.row_edges = host.loc.row_edges.data();
-        g.x0 = host.loc.x0, g.y0 = host.loc.y0, g.inv_h = host.loc.inv_h, g.ncx = host.loc.ncx, g.ncy = host.loc.ncy;
-    } else {
-        const LdsImage &I = host.lds;
-        const char *b = I.bytes.data();
-        const size_t ncell = (size_t)I.ncx * I.ncy;
-        cells64.resize(ncell);
-        for (size_t k = 0; k < ncell; ++k) cells64[k] = ((const uint32_t *)(b + I.off_cells))[k];
-        g.cells = cells64.data();
-        g.verts = (const double *)(b + I.off_verts);
-        g.poly_off = (const int32_t *)(b + I.off_poly);
-        g.row_off = (const int32_t *)(b + I.off_row_off);
-        g.row_edges = (const int32_t *)(b + I.off_row_edges);
-        g.x0 = I.x0, g.y0 = I.y0, g.inv_h = I.inv_h, g.ncx = I.ncx, g.ncy = I.ncy;
-    }
+    g.cells = host.loc.cells.data();
+    g.verts = host.loc.verts.data();
+    g.poly_off = host.loc.poly_off.data();
+    g.row_off = host.loc.row_off.data();
+    g.row_edges = host.loc.row_edges.data();
+    g.x0 = host.loc.x0, g.y0 = host.loc.y0, g.inv_h = host.loc.inv_h, g.ncx = host.loc.ncx, g.ncy = host.loc.ncy;
     for (int64_t i = 0; i < n; ++i) {
         const double x = xy[2 * i], y = xy[2 * i + 1];
         const double fx = std::floor((x - g.x0) * g.inv_h), fy = std::floor((y - g.y0) * g.inv_h);
@@ -2432,55 +1820,5 @@ const char *wgrt_status_string(wgrt_status s) {
 const char *wgrt_last_error(void) { return g_last_error.c_str(); }
 
 int wgrt_abi_version(void) { return WGRT_ABI_VERSION; }
-
-#ifdef WGRT_PHASES
-int wgrt_diag_read_phases(unsigned long long *out16, unsigned long long *wave_t) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_phase), 16 * sizeof(unsigned long long)) != hipSuccess) return 2;
-    if (hipMemcpyFromSymbol(wave_t, HIP_SYMBOL(g_phase_wave_t), sizeof(g_phase_wave_t)) != hipSuccess) return 2;
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase), z, sizeof(z));
-    std::vector<unsigned long long> zw(kPhaseWaves * 3, 0ull);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_phase_wave_t), zw.data(), sizeof(g_phase_wave_t));
-    return 0;
-}
-#endif
-
-#if defined(WGRT_DIAG) || defined(WGRT_TIMERS)
-int wgrt_diag_read_timers(unsigned long long *out8) {
-    if (hipMemcpyFromSymbol(out8, HIP_SYMBOL(g_diag_tm), 8 * sizeof(unsigned long long)) != hipSuccess) return 2;
-    unsigned long long z[8] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_tm), z, sizeof(z));
-    return 0;
-}
-#endif
-
-#ifdef WGRT_DIAG
-// Diagnostic build only: read-and-reset the wave-loop counters (synchronous).
-int wgrt_diag_read_regions(unsigned long long *out16) {
-    if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(g_diag_act), 16 * sizeof(unsigned long long)) != hipSuccess) return 2;
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_act), z, sizeof(z));
-    return 0;
-}
-
-int wgrt_diag_read_wave_times(unsigned long long *out) {   // kDiagWaves * 3, then reset
-    if (hipMemcpyFromSymbol(out, HIP_SYMBOL(g_diag_wave_t), sizeof(g_diag_wave_t)) != hipSuccess) return 2;
-    std::vector<unsigned long long> z(kDiagWaves * 3, 0ull);
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_wave_t), z.data(), sizeof(g_diag_wave_t));
-    return 0;
-}
-
-int wgrt_diag_read(unsigned long long *out17) {
-    unsigned long long h[16], fb = 0;
-    if (hipMemcpyFromSymbol(h, HIP_SYMBOL(g_diag), sizeof(h)) != hipSuccess) return 2;
-    if (hipMemcpyFromSymbol(&fb, HIP_SYMBOL(g_diag_fallback), sizeof(fb)) != hipSuccess) return 2;
-    for (int k = 0; k < 16; ++k) out17[k] = h[k];
-    out17[16] = fb;
-    unsigned long long z[16] = {0};
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag), z, sizeof(z));
-    (void)hipMemcpyToSymbol(HIP_SYMBOL(g_diag_fallback), z, sizeof(fb));
-    return 0;
-}
-#endif
 
 }  // extern "C"

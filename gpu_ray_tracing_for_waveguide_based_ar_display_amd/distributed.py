@@ -10,14 +10,15 @@ counts, so one sum-reduce of ``matrix_EB`` to rank 0 (RCCL over xGMI on MI355X, 
 the CPU tests) reproduces the single-GPU grid exactly.  That reduce is the only
 collective on the path.
 
-The tracer is pluggable (``trace_fn``) so the same sharding / reduction code runs with
-the HIP kernel in production and with the CPU oracle in the multi-process CPU tests.
+The tracer is pluggable (``trace_fn(rays, rng, eb, gid_offset, num_iter)``) so the same
+sharding / stepping / reduction code runs with the HIP kernel in production (``bench.py``,
+the reference-flow driver) and with the CPU oracle in the multi-process CPU tests.
 """
 from __future__ import annotations
 
 from dataclasses import dataclass
 
-import numpy as np
+MAX_TRACES_PER_CALL = 255   # wgrt_launch_opts.num_iter
 
 
 def block_range(n_blocks: int, world: int, rank: int) -> tuple[int, int]:
@@ -50,6 +51,35 @@ def make_shard(num_fov_x: int, num_fov_y: int, n_lambda: int, rays_per_fov: int,
     return Shard(rank, world, lo, hi, rays_per_fov)
 
 
+def split_calls(steps: int, per_call: int = 1) -> list[int]:
+    """``steps`` chained traces as calls of at most ``per_call`` traces each (0: as few calls as
+    possible), each call at most ``MAX_TRACES_PER_CALL``."""
+    if steps < 0:
+        raise ValueError("steps must be >= 0")
+    f = min(MAX_TRACES_PER_CALL, steps if per_call <= 0 else per_call) or 1
+    out = []
+    while steps > 0:
+        out.append(min(f, steps))
+        steps -= out[-1]
+    return out
+
+
+def run_steps(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: int = 1, hook=None) -> list[int]:
+    """The reference's loop of chained launches (MAIN:169-177) over one shard: ``steps`` traces
+    of every ray, each starting from the RNG states the previous one left, issued as calls of
+    at most ``per_call`` traces (``trace_fn(..., num_iter=k)``; a fused call gives the results
+    of k separate ones).  ``hook(j, "start" | "end")`` brackets call j (HIP events in bench.py).
+    Returns the traces per call."""
+    calls = split_calls(steps, per_call)
+    for j, k in enumerate(calls):
+        if hook is not None:
+            hook(j, "start")
+        trace_fn(rays, rng, eb, gid_offset, k)
+        if hook is not None:
+            hook(j, "end")
+    return calls
+
+
 def reduce_eyebox(eb, group=None, dst: int = 0):
     """Sum-reduce the eyebox grid to ``dst`` (exact: integer counts in float32 < 2**24)."""
     import torch.distributed as dist
@@ -58,30 +88,42 @@ def reduce_eyebox(eb, group=None, dst: int = 0):
     return eb
 
 
-def trace_job(shard: Shard, build_rays_fn, trace_fn, new_eb, num_iter: int = 4, group=None):
+def trace_job(shard: Shard, build_rays_fn, trace_fn, new_eb, num_iter: int = 4, per_call: int = 1, group=None):
     """Run the reference's job (``num_iter`` chained launches, MAIN:169-177) on this rank's
     shard and reduce the eyebox grid to rank 0.
 
     build_rays_fn(block_lo, block_hi) -> (rays, rng) for the shard (rng seeded with the
-    global ids); trace_fn(rays, rng, eb, gid_offset) performs one launch in place;
-    new_eb() -> zeroed eyebox grid (numpy array or torch tensor).
+    global ids); trace_fn(rays, rng, eb, gid_offset, num_iter) performs num_iter chained
+    traces in place; new_eb() -> zeroed eyebox grid (numpy array or torch tensor).
     Returns (eb, rng): eb holds the full-job grid on rank 0 (this rank's partial elsewhere).
     """
     rays, rng = build_rays_fn(shard.block_lo, shard.block_hi)
     eb = new_eb()
-    for _ in range(num_iter):
-        if shard.n_rays:
-            trace_fn(rays, rng, eb, shard.gid_offset)
+    if shard.n_rays:
+        run_steps(trace_fn, rays, rng, eb, shard.gid_offset, num_iter, per_call)
     return reduce_eyebox(eb, group), rng
 
 
-def hip_tracer(scene, variant: int = 0):
-    """trace_fn for ``trace_job`` using the HIP kernel (torch device tensors)."""
+def hip_tracer(scene, variant: int = 0, stats=None):
+    """trace_fn for ``run_steps`` / ``trace_job`` using the HIP kernel (torch device tensors);
+    ``stats`` (int64[4] device tensor) is added to by every call."""
     from .engine import trace_fullcolor
 
-    def fn(rays, rng, eb, gid_offset):
-        trace_fullcolor(scene, rays, rng, eb, gid_offset=gid_offset, variant=variant)
+    def fn(rays, rng, eb, gid_offset, num_iter=1):
+        trace_fullcolor(scene, rays, rng, eb, gid_offset=gid_offset, stats=stats, variant=variant,
+                        num_iter=num_iter)
     return fn
+
+
+def hip_shard_builder(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, device):
+    """build_rays_fn for ``trace_job`` that lays the shard out on the device (``wgrt_rays_init``,
+    MAIN:59-158 without host arrays): only the eight columns the kernel reads."""
+    from .engine import init_rays
+
+    def build(block_lo, block_hi):
+        return init_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks=(block_lo, block_hi),
+                         device=device, all_columns=False)
+    return build
 
 
 def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_lo, block_hi):
@@ -91,5 +133,5 @@ def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_l
     return rays, rng_seeds(rays["x"].shape[0], block_lo * rays_per_fov)
 
 
-__all__ = ["block_range", "Shard", "make_shard", "reduce_eyebox", "trace_job", "hip_tracer",
-           "shard_rays_host"]
+__all__ = ["block_range", "Shard", "make_shard", "split_calls", "run_steps", "reduce_eyebox", "trace_job",
+           "hip_tracer", "hip_shard_builder", "shard_rays_host", "MAX_TRACES_PER_CALL"]

@@ -18,7 +18,7 @@ from ._lib import LaunchOpts, Rays, Scene, TraceStats, WgrtError, check, load
 RAY_COLUMNS = ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 READ_COLUMNS = ("x", "y", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 
-VARIANT_AUTO, VARIANT_GRID, VARIANT_PERSISTENT = 0, 1, 2
+VARIANT_AUTO, VARIANT_GRID, VARIANT_JONES32, VARIANT_JONES64 = 0, 1, 7, 9   # include/wgrt.h
 CHUNK = 64   # rays per work-queue chunk of the persistent kernels (wgrt_launch_opts.chunk_order)
 
 

@@ -37,8 +37,8 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     import torch.distributed as dist
 
     from .couplers_coor import design_geometry
-    from .distributed import make_shard, reduce_eyebox
-    from .engine import Scene, init_rays, reserve, trace_fullcolor
+    from .distributed import hip_shard_builder, hip_tracer, make_shard, reduce_eyebox, run_steps, split_calls
+    from .engine import Scene, reserve
     from .luts import load_luts, synthetic_luts, validate_luts
     from .rays import generate_points_in_polygon
 
@@ -65,8 +65,7 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     shard = make_shard(num_FOV_x, num_FOV_y, len(lambdas), R, world, rank)
     # ray columns and RNG seeds built on the device (MAIN:59-158 without the host arrays:
     # 48 B x N of host memory and its upload at the reference's 100 x 75 x 3 x 5000 default)
-    rays, rng = init_rays(points, num_FOV_x, num_FOV_y, lambdas, R, blocks=(shard.block_lo, shard.block_hi),
-                          device=dev, all_columns=False)
+    rays, rng = hip_shard_builder(points, num_FOV_x, num_FOV_y, lambdas, R, dev)(shard.block_lo, shard.block_hi)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     stats = torch.zeros(4, dtype=torch.int64, device=dev)
     num_rays = num_FOV_x * num_FOV_y * len(lambdas) * R
@@ -74,17 +73,14 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
 
     # the num_iter chained launches of MAIN:169-177; fuse: as one call (wgrt_launch_opts.num_iter,
     # one persistent launch for the Jones-vector variants), with results identical to num_iter calls
-    calls = [1] * num_iter
-    if fuse:   # at most 255 traces per call (wgrt_launch_opts.num_iter)
-        calls = [min(255, num_iter - k) for k in range(0, num_iter, 255)]
+    per_call = 0 if fuse else 1
+    calls = split_calls(num_iter, per_call)
     if shard.n_rays and calls:
         reserve(scene, shard.n_rays, max(calls))
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0.record()
-    for k in calls:
-        if shard.n_rays:
-            trace_fullcolor(scene, rays, rng, eb, gid_offset=shard.gid_offset, stats=stats, variant=variant,
-                            num_iter=k)
+    if shard.n_rays:
+        run_steps(hip_tracer(scene, variant, stats), rays, rng, eb, shard.gid_offset, num_iter, per_call)
     t1.record()
     torch.cuda.synchronize()
     kern_s = t0.elapsed_time(t1) / 1e3

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 1
+#define WGRT_ABI_VERSION 2
 
 typedef enum {
     WGRT_OK = 0,
@@ -91,7 +91,9 @@ typedef struct {
 
 typedef struct {
     uint64_t bounces;      /* ray-bounce events: 1 in-coupling + loop iterations, per ray */
-    uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num               */
+    uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num; also fused-launch
+                              traces given up after a hand-off wait of 2^24 passes (never in a
+                              correct run: a nonzero count with in-range indices is a bug)     */
     uint64_t eyebox_hits;  /* rays accumulated into matrix_EB                             */
     uint64_t replayed;     /* Jones-vector variants: rays abandoned on an uncertain decision and
                               re-traced with the reference arithmetic (included in the counts above) */
@@ -105,8 +107,7 @@ typedef struct {
     int64_t grid_edge_cells;   /* cells whose class needs the exact polygon test      */
     int32_t n_polygons;
     int32_t device;
-    int64_t lds_locator_bytes; /* LDS image of the locator for variant 3 (0: does not fit) */
-    double lds_cell_mm;        /* its cell size                                       */
+    int64_t jtile_bytes;       /* Jones-vector tile per (lambda, FoV) (variants 7 / 9)  */
 } wgrt_scene_info;
 
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon
@@ -129,17 +130,18 @@ wgrt_status wgrt_trace_fullcolor(const wgrt_scene *scene, const wgrt_rays *rays,
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream);
 
 /* Same as wgrt_trace_fullcolor with launch tuning: kernel variant and workgroup
- * count for the persistent variants (0 = automatic).  variant: 0 auto, 1 one-ray-per-lane
- * grid, 2 persistent wave-refill (locator in global memory, 64-bit cell words), 3 persistent
- * wave-refill with a coarser copy of the locator staged in LDS, 4 variant 2 at 4 waves per
- * SIMD, 5 variant 2 with 32-bit cell words, 6 variants 4 + 5; 7 / 8 the persistent loop over
- * the Jones-vector state with certified decisions (32-bit cell words, 3 / 4 waves per SIMD),
- * 9 the same with 64-bit cell words.  Variants 7-9 re-trace the rays whose decision they cannot
- * certify with the reference arithmetic in a second kernel on the same stream
- * (wgrt_trace_stats.replayed counts them); the first such launch on a stream allocates a
- * per-stream scratch list of n_rays entries.  Variants 3, 5-8 need <= 16 polygons
- * (WGRT_ERR_UNSUPPORTED otherwise).  Auto picks 7 when possible, else 9.  All variants produce
- * identical results. */
+ * count for the persistent variants (0 = automatic).  variant:
+ *   0 auto (7 when the scene has <= 16 polygons, else 9; 1 beyond 2^32 - 1 rays);
+ *   1 one ray per lane over a ceil(N / 256) x 256 grid (the reference's launch shape) with the
+ *     reference's arithmetic;
+ *   7 the persistent wave loop over the Jones-vector state with certified decisions, 32-bit
+ *     locator cell words (<= 16 polygons, else WGRT_ERR_UNSUPPORTED);
+ *   9 the same with 64-bit cell words (<= 32 polygons).
+ * Variants 7 / 9 re-trace the rays whose decision they cannot certify with the reference
+ * arithmetic in a second kernel on the same stream (wgrt_trace_stats.replayed counts them); the
+ * first such launch on a stream allocates per-stream scratch (see wgrt_scene_reserve).  Other
+ * values (the retired variants 2-6 and 8 of ABI 1) are WGRT_ERR_INVALID_ARGUMENT.  All variants
+ * produce identical results. */
 wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays,
                                     int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
@@ -220,10 +222,9 @@ wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64
                                 uint64_t *out_mask, void *stream);
 
 /* Host-only replica of the locator (no GPU needed; test hook): builds the scene's
- * locator with cell size cell_mm (which = 0: the global-memory grid; 1: the LDS image)
- * and classifies n HOST points exactly as the kernels do. */
-wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, int which, const double *xy,
-                                       int64_t n, uint64_t *out_mask);
+ * locator with cell size cell_mm and classifies n HOST points exactly as the kernels do. */
+wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, const double *xy, int64_t n,
+                                       uint64_t *out_mask);
 
 /* Test hook: base of the Jones-vector variants' decision certification bound (default 1e-10;
  * larger values make more decisions uncertain and send more rays through the replay kernel,

@@ -40,10 +40,11 @@ def _oracle_tracer(geom, luts):
     from oracle import OracleScene
     sc = OracleScene.from_geometry(geom, luts)
 
-    def fn(rays, rng_t, eb_t, gid_offset):
+    def fn(rays, rng_t, eb_t, gid_offset, num_iter=1):
         rng = rng_t.numpy().view(np.uint32)
         eb = eb_t.numpy()
-        sc.trace(rays, rng, eb, gid_offset=gid_offset, threads=1)
+        for _ in range(num_iter):
+            sc.trace(rays, rng, eb, gid_offset=gid_offset, threads=1)
     return fn
 
 

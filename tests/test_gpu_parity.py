@@ -53,7 +53,7 @@ def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0):
 from tests._fixtures import CASES, GoldenCase  # noqa: E402
 
 
-VARIANTS = [0, 1, 2, 3, 4, 5, 6, 7, 8, 9]   # 0 = auto (what trace_fullcolor runs by default)
+VARIANTS = [0, 1, 7, 9]   # 0 = auto (what trace_fullcolor runs by default: 7 here), 1 exact grid, 9 64-bit cells
 
 
 @pytest.mark.parametrize("variant", VARIANTS)
@@ -172,7 +172,7 @@ def _trace_fused(c, dev, num_iter, variant, wavelength=None, gid_offset=0):
     return rng.cpu().numpy().view(np.uint32).copy(), eb.cpu().numpy().copy(), stats.cpu().numpy().copy()
 
 
-@pytest.mark.parametrize("variant", [0, 2, 7, 8, 9])
+@pytest.mark.parametrize("variant", [0, 1, 7, 9])
 @pytest.mark.parametrize("name", CASES)
 def test_fused_iterations_golden(dev, name, variant):
     """num_iter = 4 in one call (variants 7-9: one persistent launch running the four chained

@@ -41,10 +41,10 @@ def scene():
     return g, luts, xy, want
 
 
-@pytest.mark.parametrize("cell_mm,which", [(0.25, 0), (0.125, 0), (0.03125, 0), (0.125, 1)])
-def test_locator_equals_reference_predicate(scene, cell_mm, which):
+@pytest.mark.parametrize("cell_mm", [0.25, 0.125, 0.03125, 0.0078125])
+def test_locator_equals_reference_predicate(scene, cell_mm):
     g, luts, xy, want = scene
-    got = locator_classify_host(g, luts, xy, cell_mm=cell_mm, which=which)
+    got = locator_classify_host(g, luts, xy, cell_mm=cell_mm)
     bad = np.flatnonzero(got != want)
     assert bad.size == 0, f"{bad.size} mismatches, e.g. {xy[bad[:3]]} got {got[bad[:3]]} want {want[bad[:3]]}"
     assert want.any()
