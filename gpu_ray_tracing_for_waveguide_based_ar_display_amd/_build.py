@@ -14,7 +14,7 @@ CSRC = os.path.join(PKG, "csrc")
 REPO = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libwgrt.so")
 SOURCES = ["wgrt_trace.hip", "wgrt_scene_build.cpp"]
-HEADERS = ["wgrt_common.h", "wgrt_scene_build.h"]
+HEADERS = ["wgrt_common.h", "wgrt_device.h", "wgrt_scene.h", "wgrt_scene_build.h"]
 ARCH = os.environ.get("WGRT_OFFLOAD_ARCH", "gfx950")
 
 # -ffp-contract=off: the reference never fuses a*b+c (Python float semantics); keeping

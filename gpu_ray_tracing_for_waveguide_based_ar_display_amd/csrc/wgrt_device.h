@@ -1,0 +1,873 @@
+// wgrt_device.h -- device-side pieces shared by the bounce kernels (wgrt_trace.hip) and the
+// certification shadow (wgrt_shadow.hip): the launch arguments, the exact polygon locator, the
+// exact-arithmetic lane and the Jones-vector lane of the reference's per-ray state machine
+// (GPU_ray_tracing_functions.py = GRTF:833-1246).
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <cstddef>
+#include <cstdint>
+
+#include "../../include/wgrt.h"
+#include "wgrt_common.h"
+#include "wgrt_scene_build.h"
+
+namespace wgrt {
+
+// ----------------------------------------------------------------------------
+// device-side scene view
+// ----------------------------------------------------------------------------
+// The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t cell words (up to 32
+// polygons), uint32_t (up to 16 polygons: half the grid's cache footprint).
+template <class CellT>
+struct LocatorT {
+    using Word = CellT;
+    const CellT *cells;
+    const double *verts;
+    const int32_t *poly_off;
+    const int32_t *row_off;
+    const int32_t *row_edges;
+    double x0, y0, inv_h;
+    int ncx, ncy;
+    const double *bands;    // 128-B band records (LocatorHost::bands); NULL: CSR lists only
+};
+using Locator = LocatorT<uint64_t>;
+
+struct TraceArgs {
+    const float *x, *y, *m, *n, *l, *te, *tm, *dph;
+    uint32_t *rng;
+    float *eb;
+    wgrt_trace_stats *stats;
+    uint32_t *per_ray;
+    int64_t n_rays, gid_offset;
+    const double *tiles;
+    Locator loc;
+    int tile_d, nfc, noc, nx, ny, nl;
+    double n_g, inv_n_g;
+    double threshold;   // ener * efficiency > threshold guard of R2..R5: 0 full colour, 1e-15 single lambda
+    const int32_t *order;   // Jones-vector variants: issue order of the 64-ray chunks (NULL: ascending)
+    const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
+    int jtile_d;
+    // Jones-vector variants: out-couplings appended as (position, ray index) and binned into
+    // matrix_EB by eyebox_kernel after the launch
+    double2 *q_xy;
+    uint32_t *q_i;
+    unsigned long long *q_count;
+    double cert_tol;   // Jones-vector variants: base of the decision certification bound
+    unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
+    uint32_t *replay_list;
+    // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
+    // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
+    int n_iter;
+    uint64_t *rng64;
+    uint32_t iter_epoch;
+};
+
+// A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
+// used (a volatile scalar load, a scalar-cache hit) instead of being held in an SGPR for the
+// whole kernel: the Jones loop keeps only its per-pass operands in SGPRs; the ray columns and
+// the rare-path pointers (refill, retire, replay, out-coupling) are fetched when those run.
+// Valid only in kernels whose first parameter is the TraceArgs.
+template <class T>
+__device__ __forceinline__ T karg(size_t off) {
+    typedef volatile const T __attribute__((address_space(4))) *VP;
+    const char __attribute__((address_space(4))) *base =
+        (const char __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
+    return *(VP)(base + off);
+}
+#define KA(f) karg<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
+// the same for the locator's exact-test arrays (TraceArgs::loc holds them for every variant)
+#define KLOC(f) karg<decltype(Locator::f)>(offsetof(TraceArgs, loc) + offsetof(Locator, f))
+
+
+constexpr int kPolyEff1 = 0;
+constexpr int kPolyEff2 = 1;
+constexpr int kPolyIC = 2;
+constexpr int kPolyFC0 = 3;
+
+
+// A point's cell of the locator grid: the per-polygon class word and the cell row.
+struct Cell {
+    uint64_t w;
+    int cy;
+};
+
+template <class Loc>
+__device__ __forceinline__ Cell locate(const Loc &L, double x, double y) {
+    const double fx = floor((x - L.x0) * L.inv_h);
+    const double fy = floor((y - L.y0) * L.inv_h);
+    // NaN / out-of-grid points are outside every polygon (cell word 0 = all OUT)
+    if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return Cell{0ull, 0};
+    const int cx = (int)fx, cy = (int)fy;
+    return Cell{(uint64_t)L.cells[cy * L.ncx + cx], cy};
+}
+
+// is_inside_or_on_edge(x, y, polygon k) (GRTF:63-71): the cell class when the cell is IN or
+// OUT, else the reference predicate over the polygon's edges that meet the cell's row.
+template <class Loc>
+__device__ __forceinline__ bool in_poly(const Loc &L, const Cell &c, int k, double x, double y) {
+    const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
+    if (cls != 2u) return cls == 1u;
+    const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
+    const int r = k * L.ncy + c.cy;
+    const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
+    return inside_or_on_edge_subset(x, y, L.verts + 2 * a, nv, L.row_edges + e0, e1 - e0);
+}
+
+// First slice s in [0, count) of polygons first .. first + count - 1 containing (x, y),
+// -1 if none (the slice scans of GRTF:1002-1005 and GRTF:1112-1115, which stop at the
+// first hit).  Candidates come straight from the cell word: a slice is tested exactly only
+// when its class is EDGE; an IN slice is a hit; OUT slices are skipped.
+template <class Loc>
+__device__ __forceinline__ int first_slice(const Loc &L, const Cell &c, int first, int count,
+                                           double x, double y) {
+    uint64_t f = c.w >> (2 * first);
+    if (count < 32) f &= (1ull << (2 * count)) - 1ull;
+    const uint64_t in = f & 0x5555555555555555ull;           // class 01
+    uint64_t cand = in | ((f >> 1) & 0x5555555555555555ull);  // class 01 or 10
+    while (cand != 0ull) {
+        const int p = __builtin_ctzll(cand);
+        const int s = p >> 1;
+        if ((in >> p) & 1ull) return s;
+        if (in_poly(L, c, first + s, x, y)) return s;
+        cand &= cand - 1ull;
+    }
+    return -1;
+}
+
+// Word-only forms for the Jones-vector lane: a cell is just its class word (the row of an
+// EDGE cell is recomputed from y on the rare exact test), which keeps prefetched cells in one
+// register each.
+template <class Loc>
+__device__ __forceinline__ typename Loc::Word locate_w(const Loc &L, double x, double y) {
+    const double fx = floor((x - L.x0) * L.inv_h);
+    const double fy = floor((y - L.y0) * L.inv_h);
+    if (!(fx >= 0.0 && fy >= 0.0 && fx < (double)L.ncx && fy < (double)L.ncy)) return 0;
+    return L.cells[(int)fy * L.ncx + (int)fx];
+}
+
+template <bool KARG = false, class Loc>
+__device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y) {
+    const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
+    if (cls != 2u) return cls == 1u;
+    const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
+    const int r = k * L.ncy + cy;
+    // one 128-B record: the (at most kBandSegs) edges of polygon k meeting this cell row,
+    // evaluated with the reference predicate's operations (GRTF:36-71); NaN slots are inert
+    const double *const bands = KARG ? KLOC(bands) : L.bands;
+    const double4 *rec = (const double4 *)(bands + (size_t)r * 4 * kBandSegs);
+    const double4 s0 = rec[0], s1 = rec[1], s2 = rec[2], s3 = rec[3];
+    if (s0.x != INFINITY) {
+        bool inside = false;
+        const double4 sg[kBandSegs] = {s0, s1, s2, s3};
+#pragma unroll
+        for (int e = 0; e < kBandSegs; ++e) {
+            const double xj = sg[e].x, yj = sg[e].y, xi = sg[e].z, yi = sg[e].w;
+            if (on_segment(x, y, xj, yj, xi, yi)) return true;
+            if (((yi > y) != (yj > y)) && (x < (xj - xi) * (y - yi) / (yj - yi + 1e-20) + xi)) inside = !inside;
+        }
+        return inside;
+    }
+    const int32_t *const po = KARG ? KLOC(poly_off) : L.poly_off;
+    const int32_t *const ro = KARG ? KLOC(row_off) : L.row_off;
+    const int a = po[k], nv = po[k + 1] - a;
+    const int e0 = ro[r], e1 = ro[r + 1];
+    return inside_or_on_edge_subset(x, y, (KARG ? KLOC(verts) : L.verts) + 2 * a, nv,
+                                    (KARG ? KLOC(row_edges) : L.row_edges) + e0, e1 - e0);
+}
+
+template <bool KARG = false, class Loc>
+__device__ __forceinline__ int first_slice_w(const Loc &L, typename Loc::Word w, int first, int count, double x,
+                                             double y) {
+    uint64_t f = (uint64_t)w >> (2 * first);
+    if (count < 32) f &= (1ull << (2 * count)) - 1ull;
+    const uint64_t in = f & 0x5555555555555555ull;
+    uint64_t cand = in | ((f >> 1) & 0x5555555555555555ull);
+    while (cand != 0ull) {
+        const int p = __builtin_ctzll(cand);
+        const int sl = p >> 1;
+        if ((in >> p) & 1ull) return sl;
+        if (in_poly_w<KARG>(L, w, first + sl, x, y)) return sl;
+        cand &= cand - 1ull;
+    }
+    return -1;
+}
+
+// E_field_cal (GRTF:132-152).  rec = (p, q, r, s) complex in the reference call's argument
+// order: Ete' = p*te_in + r*tm_in, Etm' = q*te_in + s*tm_in.  The multiplications by 0.0 are
+// Python's real->complex promotions; they are kept so signed zeros propagate exactly.
+struct Field {
+    double te_re, te_im, tm_re, tm_im;
+};
+
+__device__ __forceinline__ Field efield(double Ete, double Etm, double cd, double sd, const double *rec) {
+    const double pr = rec[0], pi = rec[1], qr = rec[2], qi = rec[3];
+    const double rr = rec[4], ri = rec[5], sr = rec[6], si = rec[7];
+    const double ti_re = cd * Etm - sd * 0.0, ti_im = cd * 0.0 + sd * Etm;
+    const double a_re = pr * Ete - pi * 0.0, a_im = pr * 0.0 + pi * Ete;
+    const double b_re = rr * ti_re - ri * ti_im, b_im = rr * ti_im + ri * ti_re;
+    const double c_re = qr * Ete - qi * 0.0, c_im = qr * 0.0 + qi * Ete;
+    const double d_re = sr * ti_re - si * ti_im, d_im = sr * ti_im + si * ti_re;
+    return Field{a_re + b_re, a_im + b_im, c_re + d_re, c_im + d_im};
+}
+
+// |Ete'|^2 + |Etm'|^2 of efield() without the "* 0.0" promotion terms: for finite inputs
+// (LUTs are checked at scene creation, ray state stays finite) those terms only change the
+// sign of zero components, so every component has the same magnitude as efield()'s and the
+// sum of squares is identical.  Used for the branch estimates only.
+__device__ __forceinline__ double efield_sq(double Ete, double Etm, double cd, double sd, const double *rec) {
+    const double pr = rec[0], pi = rec[1], qr = rec[2], qi = rec[3];
+    const double rr = rec[4], ri = rec[5], sr = rec[6], si = rec[7];
+    const double ti_re = cd * Etm, ti_im = sd * Etm;
+    const double a_re = pr * Ete + (rr * ti_re - ri * ti_im), a_im = pi * Ete + (rr * ti_im + ri * ti_re);
+    const double c_re = qr * Ete + (sr * ti_re - si * ti_im), c_im = qi * Ete + (sr * ti_im + si * ti_re);
+    return (a_re * a_re + a_im * a_im) + (c_re * c_re + c_im * c_im);
+}
+
+// The ray's phase difference delta_phase is carried as its phasor (cos, sin)(delta_phase),
+// which is all E_field_cal consumes (GRTF:135: phase = complex(cos(delta), sin(delta))).
+// E_field_cal's output phase wrap(atan2(Etm') - atan2(Ete')) (GRTF:145-150; 0 for a component
+// with |.| < 1e-20) becomes the unit phasor (Etm' / |Etm'|) * conj(Ete' / |Ete'|); adding
+// lut_TIR (a taken branch) or 2 * lut_TIR (a miss hop) becomes a multiplication by its
+// phasor.  The wrap is a no-op for a phasor.  The values equal the reference's cos / sin of
+// the accumulated phase up to last-ulp rounding -- the same order as the 1-ulp differences
+// between the device's and glibc's atan2 / sin / cos that any GPU evaluation of the
+// reference's formula has (tools/math_ulps.py: atan2 differs in 27 % of calls).  A
+// Monte-Carlo decision can change only if a uniform draw lands within ~1e-16 of a branch
+// threshold (about once per 1e8 launches of the C3 batch).
+struct Phasor {
+    double c, s;
+};
+
+__device__ __forceinline__ Phasor mul(const Phasor &a, const Phasor &b) {
+    return Phasor{a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c};
+}
+
+__device__ __forceinline__ Phasor field_phasor(const Field &f, double te, double tm) {
+    const bool ue = te >= 1e-20, um = tm >= 1e-20;
+    const double er = ue ? f.te_re : 1.0, ei = ue ? f.te_im : 0.0;
+    const double mr = um ? f.tm_re : 1.0, mi = um ? f.tm_im : 0.0;
+    const double den = (ue ? te : 1.0) * (um ? tm : 1.0);
+    // (mr + i mi) * (er - i ei) / (|Etm'| |Ete'|)
+    double inv = __builtin_amdgcn_rcp(den);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    inv = fma(inv, fma(-den, inv, 1.0), inv);
+    return Phasor{(mr * er + mi * ei) * inv, (mi * er - mr * ei) * inv};
+}
+
+struct Ray {
+    double x, y, te, tm, cos_t, ener;
+    Phasor ph;   // (cos, sin) of delta_phase
+    uint32_t s;
+    int region;
+};
+
+// One ray in flight on a lane.
+struct Lane {
+    Ray r;
+    const double *T;   // this ray's (lambda, m, n) tile
+    int64_t i;         // local ray index
+    int l, m, n;
+    uint32_t bounces;  // 1 in-coupling event + loop iterations (GRTF:905)
+    bool hit;          // accumulated into matrix_EB
+};
+
+// Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
+// FoV / wavelength indices fall outside the scene.
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L) {
+    const int64_t ld = i;
+    const int m = (int)A.m[ld], n = (int)A.n[ld], l = A.l ? (int)A.l[ld] : 0;
+    if (!(m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl)) return false;
+    L.i = i;
+    L.l = l;
+    L.m = m;
+    L.n = n;
+    L.T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
+    L.r.x = (double)A.x[ld];
+    L.r.y = (double)A.y[ld];
+    L.r.te = (double)A.te[ld];
+    L.r.tm = (double)A.tm[ld];
+    {
+        double sd, cd;
+        sincos((double)A.dph[ld], &sd, &cd);
+        L.r.ph = Phasor{cd, sd};
+    }
+    L.r.cos_t = 1.0;
+    L.r.ener = 1.0;
+    L.r.s = A.rng[ld];
+    L.r.region = 0;
+    L.bounces = 1;
+    L.hit = false;
+    return true;
+}
+
+enum : int { kDie = -1, kTransit = -2 };
+constexpr int kChunk = 64;   // rays per work-queue chunk of the Jones-vector variants (chunk_order unit)
+
+
+
+// A coupler interaction: `blk` of the lane's tile, `kind` 0 in-coupler states (entry event,
+// R0, R1), 1 R2, 2 R3, 3 R4, 4 R5.  Evaluates every branch's efficiency (GRTF:860-869,
+// 909-918, ..., 1186-1200), draws, and applies the chosen branch.  Returns the next region
+// or kDie.  Only the chosen branch's phase (two atan2) is evaluated; its field is recomputed
+// by the same operations rather than kept in registers for every branch.
+template <class Loc>
+__device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane &L, int blk, int kind,
+                                        bool entry) {
+    Ray &r = L.r;
+    const double *T = L.T;
+    const double *B = T + kTileHeader + kBlock * blk;
+    double sd, cd;
+    cd = r.ph.c;
+    sd = r.ph.s;
+    const bool three = kind >= 3;
+    const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
+    const double denom = entry ? T[kTileCosIc1] : r.cos_t;
+    const double u = rng_draw(r.s, A.gid_offset + L.i);
+
+    // Decide the branch.  The reference compares u with cumulative branch efficiencies
+    // e_k = (hypot(Ete')^2 + hypot(Etm')^2) * cosA_k / cos(theta) [* or / n_g].  Here the
+    // comparisons are first made with cheap estimates (squared moduli instead of the
+    // correctly rounded hypot, one reciprocal instead of three divisions), whose relative
+    // error is below 1e-14; a decision is accepted only when every threshold it depends on
+    // is farther than 1e-12 (relative) from u and no product can underflow, which makes it
+    // provably the reference's decision.  Otherwise -- about once in 1e12 draws -- the lane
+    // recomputes every e_k exactly as the reference does.  The chosen branch's magnitudes
+    // and efficiency are always computed exactly.
+    // one branch at a time (a rolled loop keeps the register peak down)
+    double q[3] = {0.0, 0.0, 0.0};
+    const int nbr = three ? 3 : 2;
+#pragma unroll 1
+    for (int k = 0; k < nbr; ++k) {
+        const double v = efield_sq(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
+        q[0] = k == 0 ? v : q[0];
+        q[1] = k == 1 ? v : q[1];
+        q[2] = k == 2 ? v : q[2];
+    }
+    // 1 / denom to ~1e-16 relative (estimates only): hardware reciprocal + two Newton steps
+    double inv = __builtin_amdgcn_rcp(denom);
+    inv = fma(inv, fma(-denom, inv, 1.0), inv);
+    inv = fma(inv, fma(-denom, inv, 1.0), inv);
+    double a0 = q[0] * B[0] * inv, a1 = q[1] * B[1] * inv;
+    if (entry) {
+        a0 *= A.n_g;
+        a1 *= A.n_g;
+    }
+    const double a2 = three ? q[2] * B[2] * inv * A.inv_n_g : 0.0;
+    const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
+    const double scale = fabs(a0) + fabs(a1) + fabs(a2);   // bounds every partial sum
+    const double tol = 1e-12 * scale;
+    const bool tiny = thr && !(r.ener > 1e-200 && (a0 == 0.0 || a0 > 1e-100) && (a1 == 0.0 || a1 > 1e-100) &&
+                               (!three || a2 == 0.0 || a2 > 1e-100));
+    // ener * e_k > threshold (GRTF:606 single-lambda: 1e-15; GRTF:1020 full colour: 0).  With
+    // threshold 0 and no underflow it is e_k > 0, i.e. a_k > 0; otherwise the estimate
+    // ener * a_k must clear the threshold by a relative margin far above its error.
+    const double t = A.threshold;
+    const double p0 = r.ener * a0, p1 = r.ener * a1, p2 = r.ener * a2;
+    const double tmar = 1e-12 * t;
+    const bool tsure = !thr || t == 0.0 ||
+                       (fabs(p0 - t) > tmar && fabs(p1 - t) > tmar && (!three || fabs(p2 - t) > tmar));
+    const bool pass0 = !thr || (t == 0.0 ? a0 > 0.0 : p0 > t);
+    const bool pass1 = !thr || (t == 0.0 ? a1 > 0.0 : p1 > t);
+    const bool pass2 = t == 0.0 ? a2 > 0.0 : p2 > t;
+    const bool sure = scale > 1e-290 && !tiny && tsure && fabs(u - c0) > tol && fabs(u - c1) > tol &&
+                      (!three || fabs(u - c2) > tol);
+    int b;
+    if (sure) {
+        if (u <= c0 && pass0) b = 0;
+        else if (u <= c1 && pass1) b = 1;
+        else if (three && u <= c2 && pass2) b = 2;
+        else return kDie;
+    } else {
+        double te[3], tm[3];
+#pragma unroll
+        for (int k = 0; k < 3; ++k) {
+            te[k] = tm[k] = 0.0;
+            if (k < 2 || three) {
+                const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * k);
+                te[k] = hypot_cr(f.te_re, f.te_im);
+                tm[k] = hypot_cr(f.tm_re, f.tm_im);
+            }
+        }
+        double e0 = (te[0] * te[0] + tm[0] * tm[0]) * B[0] / denom;
+        double e1 = (te[1] * te[1] + tm[1] * tm[1]) * B[1] / denom;
+        if (entry) {
+            e0 = e0 * A.n_g;
+            e1 = e1 * A.n_g;
+        }
+        double e2 = 0.0;
+        if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
+        if (u <= e0 && (!thr || r.ener * e0 > t)) b = 0;
+        else if (u <= e0 + e1 && (!thr || r.ener * e1 > t)) b = 1;
+        else if (three && u <= e0 + e1 + e2 && r.ener * e2 > t) b = 2;
+        else return kDie;
+    }
+
+    if (b == 2) {  // out-coupling (GRTF:1162-1171, 1231-1240)
+        if (inside_or_on_edge(r.x, r.y, T + kTileEbRect, 4)) {
+            const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
+            const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
+            const double dx = (xmax - xmin) / kEbNx, dy = (ymax - ymin) / kEbNy;
+            int64_t ix = (int64_t)floor((r.x - xmin) / dx);
+            int64_t iy = (int64_t)floor((r.y - ymin) / dy);
+            // compiled-numba addressing (GRTF:164): a negative index wraps once, an index
+            // equal to the axis length aliases into the next row; guarded to the buffer
+            if (ix < 0) ix += kEbNx;
+            if (iy < 0) iy += kEbNy;
+            const int64_t off = ((((int64_t)L.l * A.ny + L.n) * A.nx + L.m) * kEbNy + iy) * kEbNx + ix;
+            const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
+            if (off >= 0 && off < total) {
+                unsafeAtomicAdd(A.eb + off, 1.0f);
+                L.hit = true;
+            }
+        }
+        return kDie;
+    }
+    const Field f = efield(r.te, r.tm, cd, sd, B + kBlockRec + 8 * b);
+    const double cte = hypot_cr(f.te_re, f.te_im);
+    const double ctm = hypot_cr(f.tm_re, f.tm_im);
+    double e = (cte * cte + ctm * ctm) * B[b] / denom;   // exact e_b (GRTF:868-869, 917-918, ...)
+    if (entry) e = e * A.n_g;
+    // take the branch (GRTF:872-882 and every branch body after it)
+    const double norm = sqrt(cte * cte + ctm * ctm);
+    const Phasor ph = field_phasor(f, cte, ctm);
+    int tir, gap;
+    if (kind == 0) { tir = b == 0 ? 0 : 2; gap = b == 0 ? 0 : 4; }
+    else if (kind <= 2) { tir = b == 0 ? 0 : 1; gap = b == 0 ? 0 : 2; }
+    else { tir = b == 0 ? 1 : 3; gap = b == 0 ? 2 : 6; }
+    r.cos_t = B[b];
+    r.te = cte / norm;
+    r.tm = ctm / norm;
+    r.ph = mul(ph, Phasor{T[kTileTirRot + 2 * tir], T[kTileTirRot + 2 * tir + 1]});
+    r.x += T[kTileGap + gap];
+    r.y += T[kTileGap + gap + 1];
+    r.ener = r.ener * e;
+    if (kind == 0) {
+        const bool in_ic = in_poly(loc, locate(loc, r.x, r.y), kPolyIC, r.x, r.y);
+        if (b == 0) return in_ic ? 0 : 2;
+        return in_ic ? 1 : kDie;
+    }
+    if (kind <= 2) return b == 0 ? 2 : 3;
+    return b == 0 ? 4 : 5;
+}
+
+// Run a ray through the loop iterations that need no Monte-Carlo interaction -- hops that
+// miss every coupler slice (GRTF:1049-1052, 1102-1108, 1175-1178) and the R3 -> R4 switch
+// -- until the next interaction is due.  Returns that interaction's block index, or kDie
+// when the ray terminated (left eff_reg1 at GRTF:906, R5 miss at GRTF:1244-1246, or
+// range(1e5) exhausted).  Each iteration counts one bounce.
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane &L, int &kind) {
+    Ray &r = L.r;
+    const double *T = L.T;
+    // A miss hop's step is fixed by the region: R2 moves by gap[0:2] and adds 2*TIR[0],
+    // R3 and R4 move by gap[2:4] and add 2*TIR[1] (R5 misses die).  Fetch it once.
+    // (kTileHopRot + g holds the phasor of 2*TIR[g / 2].)
+    const int g = (r.region == 2) ? 0 : 2;
+    const double gx = T[kTileGap + g], gy = T[kTileGap + g + 1];
+    const Phasor hop{T[kTileHopRot + g], T[kTileHopRot + g + 1]};   // 2 * TIR[g / 2]
+    for (;;) {
+        if (L.bounces > (uint32_t)kMaxLoop) return kDie;
+        ++L.bounces;
+        const Cell c = locate(loc, r.x, r.y);
+        if (!in_poly(loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        const int region = r.region;
+        if (region <= 1) {
+            kind = 0;
+            return 1 + region;
+        }
+        int s;
+        if (region <= 3) {
+            s = first_slice(loc, c, kPolyFC0, A.nfc, r.x, r.y);
+            if (s >= 0) {
+                kind = region - 1;
+                return 3 + (region - 2) * A.nfc + s;
+            }
+            if (region == 3 && !in_poly(loc, c, kPolyEff2, r.x, r.y)) {
+                r.region = 4;   // GRTF:1103-1104: switch to the out-coupler state without moving
+                continue;
+            }
+        } else {
+            s = first_slice(loc, c, kPolyFC0 + A.nfc, A.noc, r.x, r.y);
+            if (s >= 0) {
+                kind = region - 1;
+                return 3 + 2 * A.nfc + (region - 4) * A.noc + s;
+            }
+            if (region == 5) return kDie;
+        }
+        r.x += gx;
+        r.y += gy;
+        r.ph = mul(r.ph, hop);
+    }
+}
+
+// Eyebox accumulation of an out-coupling (GRTF:1162-1171, 1231-1240): the per-FoV
+// eyebox rectangle test, the bin, and the atomic; compiled-numba addressing as in interact().
+__device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int n, double x, double y) {
+    const double *T = A.tiles + (int64_t)((l * A.nx + m) * A.ny + n) * A.tile_d;
+    if (!inside_or_on_edge(x, y, T + kTileEbRect, 4)) return false;
+    const double xmin = T[kTileEbRange], xmax = T[kTileEbRange + 1];
+    const double ymin = T[kTileEbRange + 2], ymax = T[kTileEbRange + 3];
+    const double dx = (xmax - xmin) / kEbNx, dy = (ymax - ymin) / kEbNy;
+    int64_t ix = (int64_t)floor((x - xmin) / dx);
+    int64_t iy = (int64_t)floor((y - ymin) / dy);
+    if (ix < 0) ix += kEbNx;
+    if (iy < 0) iy += kEbNy;
+    const int64_t off = ((((int64_t)l * A.ny + n) * A.nx + m) * kEbNy + iy) * kEbNx + ix;
+    const int64_t total = (int64_t)A.nl * A.ny * A.nx * kEbNy * kEbNx;
+    if (off < 0 || off >= total) return false;
+    unsafeAtomicAdd(A.eb + off, 1.0f);
+    return true;
+}
+
+// ----------------------------------------------------------------------------
+// Jones-vector path (variants 7-9): certified decisions, side-effect-free abandon + replay
+// ----------------------------------------------------------------------------
+// The reference carries a ray's polarisation as (|Ete|, |Etm|, delta_phase) and re-derives it
+// at every taken branch through hypot, atan2 and a wrap (E_field_cal, GRTF:132-152; the
+// branch bodies GRTF:872-882, ...).  Up to a global phase that triple is the Jones vector
+// E = (|Ete|, |Etm| e^{i delta}): E_field_cal applies a 2x2 complex matrix to it, the branch
+// efficiencies are |M E|^2 times a cosine ratio, and taking a branch normalises M E and turns
+// its TM component by e^{i lut_TIR} (a miss hop by e^{2 i lut_TIR}).  These variants carry E
+// itself -- no hypot, atan2, wrap, sin or cos per interaction, one reciprocal square root for
+// the normalisation -- and keep every Monte-Carlo decision the reference's by certifying it:
+// a decision is taken only when the draw lies farther from every branch threshold than a bound
+// on the difference between this arithmetic and the reference's,
+//     tol = D * |1 / cos(theta)| * max(|E|^2, 1) * sum_k W[k]     (W[k]: wgrt_common.h kBlockW),
+//     D   = cert_tol * (1 + G (bounces / 100)^2),
+// where cert_tol (1e-10) covers the per-step rounding of both evaluations with a wide margin and
+// the quadratic term the reference's phase, which grows without a wrap over miss hops (G: the
+// tile's max |lut_TIR| / pi).  A ray whose decision cannot be certified (about one in 1e9
+// decisions) is abandoned with no side effect -- its RNG state, counters and eyebox cells are
+// written only when it terminates -- and re-traced from its launch-start state by the
+// reference-arithmetic path (replay_kernel).  Positions, hop counts and eyebox indices are the
+// reference's exact float64 operations, as in every other variant.
+//
+// Latency and issue: a ray's bounces form one dependent chain (cell word -> block -> math ->
+// next position) and a launch's tail is the chain of its longest-lived rays, so every pass is
+// built to wait for one batch of loads: an interaction loads its whole block (the TIR step of
+// each taken branch is pre-folded into the block's TM rows, wgrt_common.h kJ*), the two
+// candidate moves, and issues the cell-word loads of both candidate next positions; a miss hop
+// only moves (its phase steps are applied as a power at the next interaction) and issues the
+// cell load of its new position, read in the next pass (JLane::pf).  Out-coupled
+// rays are queued (position + ray index) and binned into matrix_EB by the epilogue kernel, so
+// the eyebox predicate and its divisions stay out of the wave loop.
+struct JRay {
+    double x, y;
+    double er, ei, mr, mi;   // Jones vector (Ete, Etm), up to a global phase
+    double cos_t, ener;
+    double eerr;             // relative error bound of ener (threshold > 0 kernels only)
+    double gx, gy;           // miss-hop move of the current region
+    uint32_t hops;           // miss hops since the last interaction (phase steps not yet applied)
+    uint32_t s;
+    int region;
+};
+
+struct JLane {
+    JRay r;
+    const double *T;         // this ray's Jones tile
+    int64_t i;
+    uint32_t bounces;
+    uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
+    uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
+    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
+};
+
+enum : int { kUncertain = -3, kOut = -4 };
+
+// The Jones-vector lane combines per-lane predicates with & and | on purpose: no short-circuit,
+// so the decision is straight-line code instead of nested divergent branches.
+#pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
+
+// Every column load is issued before anything branches on a loaded value, so a refill waits
+// for one memory round trip (not one for the FoV / wavelength indices and another for the
+// rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
+                                          uint64_t *gword = nullptr) {
+    const int64_t ld = i;
+    const float *const cl = KA(l);
+    const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
+    const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
+    const uint32_t rs = KA(rng)[ld];
+    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int m = (int)fm, n = (int)fn, l = (int)fl;
+    const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
+    L.i = i;
+    L.T = KA(jtiles) + (ok ? (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d : 0);
+    L.r.x = (double)fx;
+    L.r.y = (double)fy;
+    const double te = (double)fte, tm = (double)ftm;
+    double sd = 0.0, cd = 1.0;
+    if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
+    // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
+    L.r.er = te;
+    L.r.ei = 0.0;
+    L.r.mr = cd * tm;
+    L.r.mi = sd * tm;
+    L.r.cos_t = 1.0;
+    L.r.ener = 1.0;
+    L.r.eerr = 0.0;
+    L.r.gx = L.r.gy = 0.0;
+    L.r.hops = 0;
+    L.r.s = rs;
+    L.r.region = 0;
+    L.bounces = 1;
+    L.pf = 0ull;
+    return ok;
+}
+
+struct JField {
+    double er, ei, mr, mi;
+};
+
+struct Rec {
+    double pr, pi, qr, qi, rr, ri, sr, si;
+};
+
+__device__ __forceinline__ Rec load_rec(const double *p) {
+    const double2 a = *(const double2 *)p, b = *(const double2 *)(p + 2);
+    const double2 c = *(const double2 *)(p + 4), d = *(const double2 *)(p + 6);
+    return Rec{a.x, a.y, b.x, b.y, c.x, c.y, d.x, d.y};
+}
+
+// M E for the coefficients (p, q, r, s) of one E_field_cal call (GRTF:139-144):
+// Ete' = p Ete + r Etm, Etm' = q Ete + s Etm.
+__device__ __forceinline__ JField jones(const Rec &c, const JRay &r) {
+    JField f;
+    f.er = fma(c.pr, r.er, fma(-c.pi, r.ei, fma(c.rr, r.mr, -c.ri * r.mi)));
+    f.ei = fma(c.pr, r.ei, fma(c.pi, r.er, fma(c.rr, r.mi, c.ri * r.mr)));
+    f.mr = fma(c.qr, r.er, fma(-c.qi, r.ei, fma(c.sr, r.mr, -c.si * r.mi)));
+    f.mi = fma(c.qr, r.ei, fma(c.qi, r.er, fma(c.sr, r.mi, c.si * r.mr)));
+    return f;
+}
+
+__device__ __forceinline__ double norm2(const JField &f) {
+    return fma(f.er, f.er, fma(f.ei, f.ei, fma(f.mr, f.mr, f.mi * f.mi)));
+}
+
+// 1 / d and 1 / sqrt(v) to ~1 ulp: hardware estimate + two Newton steps.
+__device__ __forceinline__ double rcp_nr(double d) {
+    double y = __builtin_amdgcn_rcp(d);
+    y = fma(y, fma(-d, y, 1.0), y);
+    return fma(y, fma(-d, y, 1.0), y);
+}
+
+__device__ __forceinline__ double rsq_nr(double v) {
+    double y = __builtin_amdgcn_rsq(v);
+    const double h = 0.5 * v;
+    y = y * fma(-h * y, y, 1.5);
+    return y * fma(-h * y, y, 1.5);
+}
+
+// Cell word of (x, y): the grid has a border of all-OUT cells, so clamping is exact for points
+// outside it (and for NaN, which converts to 0).
+template <class Loc>
+__device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, double y) {
+    int ix = (int)((x - L.x0) * L.inv_h), iy = (int)((y - L.y0) * L.inv_h);
+    ix = min(max(ix, 0), L.ncx - 1);
+    iy = min(max(iy, 0), L.ncy - 1);
+    return L.cells[iy * L.ncx + ix];
+}
+
+// Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
+// kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
+// of it has been written) and replayed.
+template <class Loc>
+__device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
+                                        bool entry) {
+    JRay &r = L.r;
+    const double *T = L.T;
+    const double *B = T + kJHeader + kJBlock * blk;
+    const bool three = kind >= 3;
+    const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
+    // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
+    // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
+    const int ga = kind >= 3 ? 2 : 0;
+    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
+    const double2 mva = *(const double2 *)(T + kJGap + ga), mvb = *(const double2 *)(T + kJGap + gb);
+    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
+    const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
+    const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
+    const Rec k0 = load_rec(B + kJBlockRec), k1 = load_rec(B + kJBlockRec + 8);
+    Rec k2{};
+    if (three) k2 = load_rec(B + kJBlockRec + 16);
+    const double xa = r.x + mva.x, ya = r.y + mva.y;
+    const double xb = r.x + mvb.x, yb = r.y + mvb.y;
+    const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
+
+    // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
+    for (uint32_t h = 0; h < r.hops; ++h) {
+        const double mr = r.mr;
+        r.mr = fma(mr, hop.x, -r.mi * hop.y);
+        r.mi = fma(mr, hop.y, r.mi * hop.x);
+    }
+    r.hops = 0;
+    const double denom = entry ? cg.x : r.cos_t;
+    const double u = rng_draw(r.s, A.gid_offset + L.i);
+    const JField f0 = jones(k0, r), f1 = jones(k1, r);
+    const double q0 = norm2(f0), q1 = norm2(f1);
+    const double q2 = three ? norm2(jones(k2, r)) : 0.0;
+    const double inv = rcp_nr(denom);
+    const double f01 = entry ? A.n_g : 1.0;
+    const double a0 = q0 * cw.x * inv * f01, a1 = q1 * cw.y * inv * f01;
+    const double a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
+    const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
+    const double nb = (double)L.bounces * 0.01;
+    const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
+    const double scl = A.cert_tol * fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double tol = scl * cw.w;
+    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic.
+    // Non-short-circuit (&, |) throughout: one straight-line evaluation per lane.
+    bool ok = (tol > 1e-250) & (fabs(u - c0) > tol) & (fabs(u - c1) > tol) & (!three | (fabs(u - c2) > tol));
+    const double t = A.threshold;
+    bool p0 = true, p1 = true, p2 = true;
+    if (t == 0.0) {   // full colour (uniform branch)
+        // a branch the certified draw selects has e_k > tol (it lies between two thresholds more
+        // than tol from the draw), so ener * e_k > 0 holds for the reference too unless that
+        // product could underflow
+        ok = ok & (!thr | (r.ener * tol > 1e-290));
+    } else if (thr) {
+        {
+            // ener * e_k > threshold (GRTF:606): certified with ener's tracked relative error
+            const double g0 = r.ener * a0, g1 = r.ener * a1, g2 = r.ener * a2;
+            const double re = r.eerr + 1e-15;
+            const double m0 = re * fabs(g0) + r.ener * scl * B[kJBlockW] * 1.01;
+            const double m1 = re * fabs(g1) + r.ener * scl * B[kJBlockW + 1] * 1.01;
+            const double m2 = re * fabs(g2) + r.ener * scl * B[kJBlockW + 2] * 1.01;
+            p0 = g0 > t;
+            p1 = g1 > t;
+            p2 = g2 > t;
+            ok = ok && (u > c0 || fabs(g0 - t) > m0) && (u > c1 || fabs(g1 - t) > m1) &&
+                 (!three || u > c2 || fabs(g2 - t) > m2);
+        }
+    }
+    const bool s0 = (u <= c0) & p0;
+    const bool s1 = !s0 & (u <= c1) & p1;
+    const bool s2 = !s0 & !s1 & three & (u <= c2) & p2;   // out-coupling (GRTF:1162-1171, 1231-1240)
+    const bool ba = s0;
+    const JField f = ba ? f0 : f1;
+    const double n2 = ba ? q0 : q1;
+    ok = ok & (!(s0 | s1) | (n2 > 1e-300));
+    // one exit for every outcome but a taken branch; an out-coupling is appended to the
+    // out-coupling queue by the caller (at (r.x, r.y))
+    const int code = !ok ? kUncertain : s2 ? kOut : !(s0 | s1) ? kDie : 0;
+    if (code != 0) return code;
+    const int b = ba ? 0 : 1;
+    // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
+    const double rn = rsq_nr(n2);
+    r.er = f.er * rn;
+    r.ei = f.ei * rn;
+    r.mr = f.mr * rn;
+    r.mi = f.mi * rn;
+    const double ab = ba ? a0 : a1;
+    if (thr && t != 0.0) r.eerr += scl * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+    r.ener = r.ener * ab;
+    r.cos_t = ba ? cw.x : cw.y;
+    r.x = ba ? xa : xb;
+    r.y = ba ? ya : yb;
+    r.gx = ba ? mva.x : mvb.x;
+    r.gy = ba ? mva.y : mvb.y;
+    L.pf = ba ? pa : pb;
+    if (kind == 0) {
+        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
+        if (ba) return in_ic ? 0 : 2;
+        return in_ic ? 1 : kDie;
+    }
+    if (kind <= 2) return ba ? 2 : 3;
+    return ba ? 4 : 5;
+}
+
+// Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
+// that need no Monte-Carlo interaction, at most kJMaxHops per call: every iteration then tests
+// a cell word loaded a pass earlier, L.pf, and a hop issues the load of the next one.  1 measured
+// best on C3 (2 and 4 slower); a compile-time bound, not a kernarg, straightens the loop (-2 %
+// fused).
+constexpr int kJMaxHops = 1;
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+    JRay &r = L.r;
+    for (int hops = 0;; ++hops) {
+        if (hops >= kJMaxHops) return kTransit;
+        if (L.bounces > (uint32_t)kMaxLoop) return kDie;
+        ++L.bounces;
+        const auto c = (typename Loc::Word)L.pf;
+        if (!in_poly_w<true>(loc, c, kPolyEff1, r.x, r.y)) return kDie;
+        const int region = r.region;
+        if (region <= 1) {
+            kind = 0;
+            return 1 + region;
+        }
+        // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
+        const bool fc = region <= 3;
+        const int first = fc ? kPolyFC0 : kPolyFC0 + A.nfc, count = fc ? A.nfc : A.noc;
+        const int s = first_slice_w<true>(loc, c, first, count, r.x, r.y);
+        if (s >= 0) {
+            kind = region - 1;
+            return (fc ? 3 + (region - 2) * A.nfc : 3 + 2 * A.nfc + (region - 4) * A.noc) + s;
+        }
+        if (region == 5) return kDie;   // GRTF:1244-1246
+        if (region == 3 && !in_poly_w<true>(loc, c, kPolyEff2, r.x, r.y)) {
+            r.region = 4;   // GRTF:1103-1104: no move, same miss hop (gap[2:4], 2 TIR[1])
+            continue;
+        }
+        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178); its phase step waits for the next interaction
+        r.x = r.x + r.gx;
+        r.y = r.y + r.gy;
+        ++r.hops;
+        L.pf = locate_c(loc, r.x, r.y);   // used from the next pass on
+    }
+}
+
+template <class LaneT>
+__device__ __forceinline__ void lane_retire(const TraceArgs &A, const LaneT &L) {
+    A.rng[L.i] = L.r.s;
+    if (A.per_ray) A.per_ray[L.i] = L.bounces;
+}
+
+__device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
+    for (int off = 32; off > 0; off >>= 1) v += __shfl_xor(v, off);
+    return v;
+}
+
+// Per-wave reduction of the ray counters, then one 64-bit atomic per counter per wave.
+__device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t bounces, uint64_t hits,
+                                          uint64_t bad) {
+    bounces = wave_sum(bounces);
+    hits = wave_sum(hits);
+    bad = wave_sum(bad);
+    if ((threadIdx.x & 63) == 0 && stats) {
+        if (bounces) atomicAdd((unsigned long long *)&stats->bounces, (unsigned long long)bounces);
+        if (hits) atomicAdd((unsigned long long *)&stats->eyebox_hits, (unsigned long long)hits);
+        if (bad) atomicAdd((unsigned long long *)&stats->bad_rays, (unsigned long long)bad);
+    }
+}
+
+// Trace ray i to termination with the reference arithmetic (variant 1's lane; replays).  With
+// s_io, the trace starts from *s_io instead of rng_states[i] and leaves its final state there
+// (rng_states untouched).
+__device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad,
+                                          uint32_t *s_io = nullptr) {
+    Lane L;
+    if (!lane_load(A, i, L)) {
+        ++bad;
+        return;
+    }
+    if (s_io) L.r.s = *s_io;
+    int blk = 0, kind = 0;
+    bool entry = true;
+    for (;;) {
+        const int next = interact(A, A.loc, L, blk, kind, entry);
+        if (next < 0) break;
+        L.r.region = next;
+        entry = false;
+        blk = advance(A, A.loc, L, kind);
+        if (blk < 0) break;
+    }
+    if (s_io) *s_io = L.r.s;
+    else lane_retire(A, L);
+    b += L.bounces;
+    h += L.hit;
+}
+
+}  // namespace wgrt

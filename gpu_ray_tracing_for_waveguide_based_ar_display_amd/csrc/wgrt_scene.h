@@ -1,0 +1,82 @@
+// wgrt_scene.h -- the device-resident scene behind the opaque wgrt_scene handle (include/wgrt.h),
+// shared by the C-ABI translation units.
+#pragma once
+
+#include <hip/hip_runtime.h>
+
+#include <map>
+#include <mutex>
+#include <string>
+
+#include "wgrt_device.h"
+
+struct wgrt_scene {
+    int device = 0;
+    int nx = 0, ny = 0, nl = 0, nfc = 0, noc = 0, tile_d = 0, npoly = 0;
+    double n_g = 0;
+    double *d_tiles = nullptr;
+    double *d_jtiles = nullptr;
+    int jtile_d = 0;
+    uint64_t *d_cells = nullptr;
+    uint32_t *d_cells32 = nullptr;   // 32-bit copy of the cell words (npoly <= 16), else NULL
+    double *d_verts = nullptr;
+    int32_t *d_poly_off = nullptr;
+    int32_t *d_row_off = nullptr;
+    int32_t *d_row_edges = nullptr;
+    double *d_bands = nullptr;
+    wgrt::LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
+    int64_t tiles = 0;
+    int jones_grid = 0;        // resident 256-thread workgroups of variant 7
+    int jones64_grid = 0;      // ... of variant 9
+    // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so
+    // they may share it; launches on different streams never do)
+    struct Scratch {
+        unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), replay count, queue count
+        uint32_t *list = nullptr;            // replay list
+        int64_t cap = 0;                     // replay list entries
+        double2 *q_xy = nullptr;             // out-coupling queue: position, ray index
+        uint32_t *q_i = nullptr;
+        int64_t qcap = 0;
+        uint64_t *rng64 = nullptr;           // fused launches: per-ray {state, tag} granules
+        uint32_t iter_epoch = 0;             // < 2^23 (iter_tag)
+        int64_t cap64 = 0;
+    };
+    std::mutex scratch_mu;
+    std::map<void *, Scratch> scratch;
+};
+
+namespace wgrt {
+
+// Record the detail of a failing entry point for wgrt_last_error() and return its status.
+wgrt_status fail(wgrt_status s, const std::string &msg);
+
+inline Locator make_locator(const wgrt_scene *s) {
+    Locator L;
+    L.cells = s->d_cells;
+    L.verts = s->d_verts;
+    L.poly_off = s->d_poly_off;
+    L.row_off = s->d_row_off;
+    L.row_edges = s->d_row_edges;
+    L.bands = s->d_bands;
+    L.x0 = s->loc_host.x0;
+    L.y0 = s->loc_host.y0;
+    L.inv_h = s->loc_host.inv_h;
+    L.ncx = s->loc_host.ncx;
+    L.ncy = s->loc_host.ncy;
+    return L;
+}
+
+inline LocatorT<uint32_t> make_locator32(const wgrt_scene *s) {
+    const Locator g = make_locator(s);
+    LocatorT<uint32_t> L;
+    L.cells = s->d_cells32;
+    L.verts = g.verts;
+    L.poly_off = g.poly_off;
+    L.row_off = g.row_off;
+    L.row_edges = g.row_edges;
+    L.bands = g.bands;
+    L.x0 = g.x0, L.y0 = g.y0, L.inv_h = g.inv_h, L.ncx = g.ncx, L.ncy = g.ncy;
+    return L;
+}
+
+}  // namespace wgrt
