@@ -13,7 +13,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 REPO = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libwgrt.so")
-SOURCES = ["wgrt_trace.hip", "wgrt_scene_build.cpp"]
+SOURCES = ["wgrt_trace.hip", "wgrt_shadow.hip", "wgrt_scene_build.cpp"]
 HEADERS = ["wgrt_common.h", "wgrt_device.h", "wgrt_scene.h", "wgrt_scene_build.h"]
 ARCH = os.environ.get("WGRT_OFFLOAD_ARCH", "gfx950")
 

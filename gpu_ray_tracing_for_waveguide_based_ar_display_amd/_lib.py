@@ -17,7 +17,7 @@ LIB_PATH = os.path.join(PKG, "libwgrt.so")
 ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
-            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_status_string",
+            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
 
@@ -62,6 +62,13 @@ class LaunchOpts(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_int), ("variant", ctypes.c_int), ("workgroups", ctypes.c_int),
                 ("chunk_order", ctypes.c_void_p), ("n_chunk_order", ctypes.c_int64),
                 ("num_iter", ctypes.c_int)]
+
+
+class ShadowStats(ctypes.Structure):
+    _fields_ = [("decisions", ctypes.c_uint64), ("uncertain", ctypes.c_uint64), ("silent_flips", ctypes.c_uint64),
+                ("bounces", ctypes.c_uint64), ("max_ratio", ctypes.c_double),
+                ("max_ratio_by_depth", ctypes.c_double * 6), ("decisions_by_depth", ctypes.c_uint64 * 6),
+                ("ratio_hist", ctypes.c_uint64 * 20), ("max_ener_ratio", ctypes.c_double)]
 
 
 class SceneInfo(ctypes.Structure):
@@ -118,6 +125,9 @@ def load(path: str = LIB_PATH):
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
     L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
+    L.wgrt_debug_shadow.restype = st
+    L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp, _vp,
+                                    _vp, _vp]
     L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
     L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
     L.wgrt_status_string.restype = ctypes.c_char_p

@@ -50,13 +50,20 @@ struct TraceArgs {
     const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
     int jtile_d;
     // Jones-vector variants: out-couplings appended as (position, ray index) and binned into
-    // matrix_EB by eyebox_kernel after the launch
+    // matrix_EB by the epilogue kernel after the launch
     double2 *q_xy;
     uint32_t *q_i;
     unsigned long long *q_count;
     double cert_tol;   // Jones-vector variants: base of the decision certification bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
+    // Jones-vector variants: per-wave counter partials {bounces, bad_rays, eyebox_hits, replayed}
+    // (trace-kernel waves first, then one slot per epilogue workgroup), summed into *stats by the
+    // epilogue's last workgroup -- no contended atomics on the four stats words
+    unsigned long long *part;
+    int n_trace_waves;
+    unsigned int *ticket;               // epilogue workgroups done (the last one sums and resets)
+    unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;
@@ -541,7 +548,7 @@ __device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int
 // tile's max |lut_TIR| / pi).  A ray whose decision cannot be certified (about one in 1e9
 // decisions) is abandoned with no side effect -- its RNG state, counters and eyebox cells are
 // written only when it terminates -- and re-traced from its launch-start state by the
-// reference-arithmetic path (replay_kernel).  Positions, hop counts and eyebox indices are the
+// reference-arithmetic path (the epilogue kernel).  Positions, hop counts and eyebox indices are the
 // reference's exact float64 operations, as in every other variant.
 //
 // Latency and issue: a ray's bounces form one dependent chain (cell word -> block -> math ->

@@ -77,15 +77,33 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     add_stats(A.stats, b, h, bad);
 }
 
-// Runs right behind every Jones-vector launch on its stream: bins the queued out-couplings
-// (entry j: position q_xy[j] of ray q_i[j]) into matrix_EB -- the eyebox predicate, its
-// divisions and the atomics stay out of the bounce loop.  matrix_EB cells count hits (+1.0f),
-// so the binning order does not matter.
-__global__ __launch_bounds__(256) void eyebox_kernel(TraceArgs A) {
-    uint64_t h = 0;
-    const unsigned long long nq = *A.q_count;
-    for (unsigned long long j = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; j < nq;
-         j += (unsigned long long)gridDim.x * blockDim.x) {
+// Launch scratch counters of the Jones-vector variants: kHeads work-queue heads, then the replay
+// count, the out-coupling queue count and the epilogue ticket, each on its own 128-B line.
+constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
+constexpr int kHeads = 8;
+constexpr int kScratchCtr = (kHeads + 3) * kHeadStride;   // heads, replay count, queue count, ticket
+constexpr int kScratchCtrWords = kScratchCtr;
+
+// Runs right behind every Jones-vector launch on its stream (one launch instead of three):
+//  1. bins the queued out-couplings (entry j: position q_xy[j] of ray q_i[j]) into matrix_EB --
+//     the eyebox predicate, its divisions and the atomics stay out of the bounce loop; cells
+//     count hits (+1.0f), so the binning order does not matter;
+//  2. re-traces the rays the launch abandoned (uncertain decisions; nothing of them was written)
+//     from their launch-start state with the reference arithmetic (usually none);
+//  3. its last workgroup (ticket) sums the per-wave counter partials of the trace kernel and of
+//     the epilogue workgroups into *stats -- four atomics per launch -- and zeroes the launch
+//     scratch counters (queue heads, replay / queue counts, ticket) for the next launch on the
+//     stream, which therefore needs no memset of its own.
+constexpr int kEpilogueGroups = 256;
+
+__global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
+    __shared__ unsigned long long red[4][4];
+    __shared__ bool last;
+    const unsigned long long nq = *A.q_count, nr = *A.replay_count;
+    const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
+    const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
+    uint64_t h = 0, b = 0, bad = 0;
+    for (unsigned long long j = tid; j < nq; j += nth) {
         const uint32_t qi = A.q_i[j];
         if (qi == 0xffffffffu) continue;   // a slot its wave left unused
         const int64_t i = qi;
@@ -93,18 +111,7 @@ __global__ __launch_bounds__(256) void eyebox_kernel(TraceArgs A) {
         const int m = (int)A.m[i], n = (int)A.n[i], l = A.l ? (int)A.l[i] : 0;
         h += eyebox_add(A, l, m, n, p.x, p.y);
     }
-    add_stats(A.stats, 0, h, 0);
-}
-
-// Then re-traces the rays the launch abandoned (uncertain decisions; nothing of them was
-// written) from their launch-start state with the reference arithmetic.  Usually the list is
-// empty and every workgroup exits at once.
-__global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
-    const unsigned long long nr = *A.replay_count;
-    if ((unsigned long long)blockIdx.x * blockDim.x >= nr) return;   // workgroup-uniform
-    uint64_t b = 0, h = 0, bad = 0;
-    for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr;
-         k += (unsigned long long)gridDim.x * blockDim.x) {
+    for (unsigned long long k = tid; k < nr; k += nth) {
         const int64_t i = (int64_t)A.replay_list[k];
         if (A.n_iter <= 1) {
             trace_one(A, i, b, h, bad);
@@ -115,9 +122,60 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
             A.rng[i] = st;
         }
     }
-    add_stats(A.stats, b, h, bad);
-    if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats)
-        atomicAdd((unsigned long long *)&A.stats->replayed, nr);
+    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    b = wave_sum(b);
+    bad = wave_sum(bad);
+    h = wave_sum(h);
+    if (lane == 0) {
+        red[w][0] = b;
+        red[w][1] = bad;
+        red[w][2] = h;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long *slot = A.part + 4 * ((size_t)A.n_trace_waves + blockIdx.x);
+        slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        slot[3] = 0;
+        __threadfence();   // partials visible device-wide before the ticket
+        last = atomicAdd(A.ticket, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (!last) return;
+    __threadfence();   // acquire: every other workgroup's partials and the trace waves' (kernel boundary)
+    const int nslots = A.n_trace_waves + (int)gridDim.x;
+    uint64_t s0 = 0, s1 = 0, s2 = 0;
+    for (int k = threadIdx.x; k < nslots; k += blockDim.x) {
+        const volatile unsigned long long *slot = A.part + 4 * (size_t)k;
+        s0 += slot[0];
+        s1 += slot[1];
+        s2 += slot[2];
+    }
+    s0 = wave_sum(s0);
+    s1 = wave_sum(s1);
+    s2 = wave_sum(s2);
+    __syncthreads();
+    if (lane == 0) {
+        red[w][0] = s0;
+        red[w][1] = s1;
+        red[w][2] = s2;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        wgrt_trace_stats *st = A.stats;
+        if (st) {
+            const unsigned long long t0 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+            const unsigned long long t1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+            const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+            if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
+            if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
+            if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
+            if (nr) atomicAdd((unsigned long long *)&st->replayed, nr);
+        }
+    }
+    // zero the launch scratch counters for the next launch on this stream
+    if (threadIdx.x < kScratchCtrWords) A.heads0[threadIdx.x] = 0ull;
 }
 
 // Work queue of the Jones-vector variants: one head per XCD (each on its own 128-B line), head
@@ -125,9 +183,6 @@ __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
 // of consecutive chunks (FoV x wavelength tiles stay in that XCD's L2) and the dequeue
 // atomics spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The
 // XCD id steers placement only: any wave may take any chunk, so correctness never depends on it.
-constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
-constexpr int kHeads = 8;
-constexpr int kScratchCtr = (kHeads + 2) * kHeadStride;   // heads, replay count, out-coupling slots
 constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
                                // out-couples ~10 rays per trace; unused slots cost the eyebox
                                // epilogue a read each)
@@ -352,7 +407,16 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
-    add_stats(KA(stats), tot_b, 0, tot_bad);
+    // this wave's counters go to its partial slot (summed by the epilogue: no contended atomics)
+    tot_b = wave_sum(tot_b);
+    tot_bad = wave_sum(tot_bad);
+    if (lane == 0) {
+        unsigned long long *slot = KA(part) + 4 * ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
+        slot[0] = tot_b;
+        slot[1] = tot_bad;
+        slot[2] = 0;
+        slot[3] = 0;
+    }
 }
 
 // Variants 7 / 9: the persistent loop over the Jones-vector path, 3 waves per SIMD (32-bit cell
@@ -532,6 +596,7 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
         (void)hipFree(kv.second.q_xy);
         (void)hipFree(kv.second.q_i);
         (void)hipFree(kv.second.rng64);
+        (void)hipFree(kv.second.part);
     }
     delete s;
     return WGRT_OK;
@@ -567,8 +632,21 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
     wgrt_scene::Scratch *sc = &ms->scratch[stream];
     *out = sc;
     if (!sc->ctr) {
+        // zeroed once here; afterwards every launch's epilogue leaves the counters zeroed
         hipError_t e = hipMalloc((void **)&sc->ctr, kScratchCtr * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemset(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long));
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+    }
+    // counter partials: one slot per trace-kernel wave (4 per workgroup) and per epilogue workgroup
+    const int64_t slots = grid * 4 + kEpilogueGroups;
+    if (sc->part_slots < slots) {
+        HIP_TRY(hipStreamSynchronize(st));
+        (void)hipFree(sc->part);
+        sc->part = nullptr;
+        sc->part_slots = 0;
+        hipError_t e = hipMalloc((void **)&sc->part, (size_t)slots * 4 * sizeof(unsigned long long));
+        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
+        sc->part_slots = slots;
     }
     if (sc->cap < n_rays) {
         // the old lists may still be in use by this stream's previous launch
@@ -714,7 +792,10 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.q_xy = sc->q_xy;
     A.q_i = sc->q_i;
     A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
-    HIP_TRY(hipMemsetAsync(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long), st));
+    A.ticket = (unsigned int *)(sc->ctr + (kHeads + 2) * kHeadStride);
+    A.heads0 = sc->ctr;
+    A.part = sc->part;
+    A.n_trace_waves = (int)grid * 4;
     const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
     const dim3 g3((unsigned)grid), b3(256);
     if (variant == 9) {
@@ -730,9 +811,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
             hipLaunchKernelGGL((trace_jones_kernel<uint32_t, false>), g3, b3, 0, st, A, l32, sc->ctr, jchunk);
     }
     HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(eyebox_kernel, dim3(1024), dim3(256), 0, st, A);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(replay_kernel, dim3(64), dim3(256), 0, st, A);
+    hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }

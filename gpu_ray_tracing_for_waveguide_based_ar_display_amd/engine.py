@@ -203,6 +203,41 @@ def classify_points(scene: Scene, xy: torch.Tensor, stream=None) -> torch.Tensor
     return out
 
 
+SHADOW_DEPTHS = ("[1,10)", "[10,30)", "[30,100)", "[100,300)", "[300,1000)", "[1000,inf)")
+
+
+def shadow(scene: Scene, rays: dict, rng_states: torch.Tensor, gid_offset: int = 0, n_rays: int | None = None,
+           per_ray_bounces: torch.Tensor | None = None, stream=None) -> dict:
+    """Certification shadow of the Jones-vector lane (``wgrt_debug_shadow``): traces the rays with
+    the reference's own arithmetic and measures, at every Monte-Carlo decision, how far the
+    product lane's thresholds stray from the reference's relative to its certification bound.
+    ``rng_states`` / ``per_ray_bounces`` are updated as one exact launch would.  Synchronous;
+    returns the statistics as a dict (``max_ratio``, ``silent_flips``, ``uncertain``, ...)."""
+    device = torch.device("cuda", scene.device)
+    x = rays["x"]
+    N = x.numel() if n_rays is None else int(n_rays)
+    single = scene.single_lambda
+    cols = {k: _as_dev(rays[k], torch.float32, k, device, x.numel()) for k in READ_COLUMNS
+            if not (single and k == "lmd_num")}
+    _as_dev(rng_states, rng_states.dtype, "rng_states", device, x.numel())
+    r = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in cols.items()})
+    nbytes = ctypes.sizeof(_lib.ShadowStats)
+    buf = torch.zeros(nbytes // 8, dtype=torch.int64, device=device)
+    check(load().wgrt_debug_shadow(scene.handle, ctypes.byref(r), N, int(gid_offset), int(single),
+                                   ctypes.c_void_p(rng_states.data_ptr()),
+                                   ctypes.c_void_p(per_ray_bounces.data_ptr()) if per_ray_bounces is not None else None,
+                                   ctypes.c_void_p(buf.data_ptr()), ctypes.c_void_p(_stream_handle(device, stream))),
+          "wgrt_debug_shadow")
+    host = buf.cpu().numpy()
+    st = _lib.ShadowStats.from_buffer_copy(host.tobytes())
+    return {"decisions": st.decisions, "uncertain": st.uncertain, "silent_flips": st.silent_flips,
+            "bounces": st.bounces, "max_ratio": st.max_ratio,
+            "max_ratio_by_depth": dict(zip(SHADOW_DEPTHS, list(st.max_ratio_by_depth))),
+            "decisions_by_depth": dict(zip(SHADOW_DEPTHS, [int(v) for v in st.decisions_by_depth])),
+            "ratio_hist_log10": {f"1e{b - 18}": int(v) for b, v in enumerate(st.ratio_hist) if v},
+            "max_ener_ratio": st.max_ener_ratio}
+
+
 def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor:
     """Device sqrt, div, hypot_cr, atan2, sin, cos, wrap on (a, b) -> [7, n] float64."""
     n = a.numel()
@@ -213,5 +248,5 @@ def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor
     return out
 
 
-__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "schedule_by_lifetime", "rays_to_device", "classify_points",
-           "selftest_math", "RAY_COLUMNS", "_lib"]
+__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "schedule_by_lifetime",
+           "rays_to_device", "classify_points", "shadow", "selftest_math", "RAY_COLUMNS", "_lib"]

@@ -228,8 +228,33 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
 
 /* Test hook: base of the Jones-vector variants' decision certification bound (default 1e-10;
  * larger values make more decisions uncertain and send more rays through the replay kernel,
- * results unchanged).  Process-wide; returns the previous value. */
+ * results unchanged).  Process-wide; returns the previous value (a value <= 0 only queries). */
 double wgrt_debug_set_cert_tol(double cert_tol);
+
+/* Certification shadow of the Jones-vector variants (diagnostic; wgrt_shadow.hip).  Traces rays
+ * [0, n_rays) with the reference's own arithmetic (unwrapped delta_phase, hypot / atan2 / wrap,
+ * GRTF:132-152 and 905-1246) and, at every Monte-Carlo decision, evaluates the Jones-vector lane's
+ * thresholds and certification bound tol on the same state.  rng_states (DEVICE, in/out) and the
+ * optional per_ray_bounces follow the reference's path, so they equal one launch of the exact
+ * kernel; matrix_EB is not written.  stats: DEVICE pointer, ADDED to (zero it yourself); max
+ * fields are max-combined.  single: the single-wavelength kernel (threshold 1e-15). */
+typedef struct {
+    uint64_t decisions;          /* Monte-Carlo decisions evaluated                                 */
+    uint64_t uncertain;          /* decisions the Jones lane cannot certify (its rays are replayed)   */
+    uint64_t silent_flips;       /* certified Jones decisions that differ from the reference's: 0    */
+    uint64_t bounces;            /* ray-bounce events traced                                          */
+    double max_ratio;            /* max over decisions / thresholds of |c_jones - c_ref| / tol        */
+    double max_ratio_by_depth[6];   /* the same by bounce depth [1,10) [10,30) [30,100) [100,300)
+                                       [300,1000) [1000,inf)                                          */
+    uint64_t decisions_by_depth[6];
+    uint64_t ratio_hist[20];     /* decisions by log10 of their max ratio: bucket b = [1e(b-18),
+                                    1e(b-17)); bucket 0 also holds smaller ratios, 19 larger ones    */
+    double max_ener_ratio;       /* single wavelength: max |ener_jones / ener_ref - 1| / tracked bound */
+} wgrt_shadow_stats;
+
+wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
+                              int single, uint32_t *rng_states, uint32_t *per_ray_bounces, wgrt_shadow_stats *stats,
+                              void *stream);
 
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */

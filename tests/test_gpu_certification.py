@@ -1,0 +1,157 @@
+"""Pins the Jones-vector path where it is weakest: its certification bound and the deep configs.
+
+* The certification shadow (``wgrt_debug_shadow``, csrc/wgrt_shadow.hip) traces rays with the
+  reference's own arithmetic -- unwrapped delta_phase, hypot / atan2 / wrap (GRTF:132-152),
+  ``delta_phase += 2 * lut_TIR`` over miss hops (GRTF:1052, 1108, 1178) -- and evaluates the
+  product lane's thresholds and bound ``tol`` on the same state at every decision.  Measured:
+  ``max |c_jones - c_ref| / tol`` must stay <= 1e-2 (the bound is >= 100x the error it covers)
+  and no certified decision may differ from the reference's (``silent_flips == 0``), at the C3
+  and C5 sizes and on the single-wavelength deep-bounce guard case.  The statistics are written
+  to ``$WGRT_RESULTS_DIR`` (default ``gpurun_out/``) for DESIGN.md.
+* C5 (41x41x3x16384, deep-bounce LUT) and the reference's default job (100x75x3x5000,
+  MAIN:16-17, 60-61) against the CPU oracle on sampled FoV x wavelength blocks: rays are
+  independent and blocks write disjoint eyebox slabs, so a sample of blocks traced by the oracle
+  with ``gid_offset`` must match the full GPU launch exactly (per-ray bounces, RNG, slabs).
+
+Tolerance: exact equality for every traced quantity; the 1e-2 ratio is the certification margin.
+"""
+import json
+import os
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+RESULTS = os.environ.get("WGRT_RESULTS_DIR", os.path.join(os.path.dirname(os.path.dirname(__file__)), "gpurun_out"))
+
+
+@pytest.fixture(scope="module")
+def dev():
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    return torch.device("cuda", 0)
+
+
+def _setup(nx, ny, lambdas, R, profile="default", seed=0, gap_scale=1.0, wavelength=None):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+    geom = design_geometry(nx, ny)
+    geom.lut_gap = geom.lut_gap * gap_scale
+    luts = synthetic_luts(geom, seed=seed, profile=profile)
+    pts = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
+    return geom, luts, pts
+
+
+def _record(name, stats):
+    os.makedirs(RESULTS, exist_ok=True)
+    path = os.path.join(RESULTS, "certification_shadow.json")
+    data = {}
+    if os.path.exists(path):
+        try:
+            data = json.load(open(path))
+        except ValueError:
+            data = {}
+    data[name] = stats
+    json.dump(data, open(path, "w"), indent=1)
+
+
+def _shadow_run(dev, nx, ny, lambdas, R, **kw):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, init_rays, shadow
+    wl = kw.get("wavelength")
+    geom, luts, pts = _setup(nx, ny, lambdas, R, **kw)
+    scene = Scene.from_geometry(geom, luts, wavelength=wl)
+    rays, rng = init_rays(pts, nx, ny, lambdas, R, device=dev, all_columns=False)
+    per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
+    st = shadow(scene, rays, rng, per_ray_bounces=per)
+    scene.close()
+    return st, geom, luts, pts, rng, per
+
+
+def test_shadow_follows_reference(dev):
+    """The shadow's reference lane is the reference: its RNG states and bounce counts equal the
+    CPU oracle's (pinned to the golden fixtures) on a deep-bounce LUT."""
+    from oracle import OracleScene
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
+    nx, ny, lam, R = 9, 7, [0, 1, 2], 512
+    st, geom, luts, pts, rng, per = _shadow_run(dev, nx, ny, lam, R, profile="deep", seed=5)
+    rays = build_rays(pts, nx, ny, lam, R)
+    orng = rng_seeds(rays["x"].shape[0])
+    eb = np.zeros((3, ny, nx, 80, 120), np.float32)
+    tot, cnt = OracleScene.from_geometry(geom, luts).trace(rays, orng, eb, per_ray_bounces=True)
+    np.testing.assert_array_equal(rng.cpu().numpy().view(np.uint32), orng)
+    np.testing.assert_array_equal(per.cpu().numpy().view(np.uint32), cnt)
+    assert st["bounces"] == tot
+    assert st["silent_flips"] == 0
+
+
+@pytest.mark.parametrize("name,cfg", [
+    ("C3", dict(nx=21, ny=21, lambdas=[0, 1, 2], R=1024)),
+    ("C5", dict(nx=41, ny=41, lambdas=[0, 1, 2], R=16384, profile="deep")),
+    ("single_lambda_guard", dict(nx=7, ny=7, lambdas=[2], R=4096, profile="balanced", gap_scale=0.25,
+                                 wavelength=2)),
+])
+def test_certification_slack(dev, name, cfg):
+    st, *_ = _shadow_run(dev, **cfg)
+    _record(name, st)
+    print(name, json.dumps(st))
+    assert st["decisions"] > 0
+    assert st["silent_flips"] == 0
+    assert st["max_ratio"] <= 1e-2, st
+    if cfg.get("wavelength") is not None:
+        assert st["max_ener_ratio"] <= 1e-2, st
+
+
+def _blocks_vs_oracle(dev, nx, ny, lambdas, R, sample, profile="default", threads=16):
+    """Full GPU launch (product variant) vs the oracle on the sampled FoV x wavelength blocks."""
+    from oracle import OracleScene
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, init_rays, trace_fullcolor
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
+    geom, luts, pts = _setup(nx, ny, lambdas, R, profile=profile)
+    scene = Scene.from_geometry(geom, luts)
+    rays, rng = init_rays(pts, nx, ny, lambdas, R, device=dev, all_columns=False)
+    per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    trace_fullcolor(scene, rays, rng, eb, per_ray_bounces=per, stats=stats)
+    torch.cuda.synchronize()
+    scene.close()
+    del rays
+    osc = OracleScene.from_geometry(geom, luts)
+    oeb = np.zeros(osc.eb_shape(), np.float32)
+    L = len(lambdas)
+    for b in sample:
+        lo, hi = b * R, (b + 1) * R
+        hr = build_rays(pts, nx, ny, lambdas, R, blocks=(b, b + 1))
+        orng = rng_seeds(R, lo)
+        _, cnt = osc.trace(hr, orng, oeb, gid_offset=lo, threads=threads, per_ray_bounces=True)
+        np.testing.assert_array_equal(per[lo:hi].cpu().numpy().view(np.uint32), cnt, err_msg=f"block {b}")
+        np.testing.assert_array_equal(rng[lo:hi].cpu().numpy().view(np.uint32), orng, err_msg=f"block {b}")
+        fov, k = divmod(b, L)
+        m, n = divmod(fov, ny)
+        l = lambdas[k]
+        np.testing.assert_array_equal(eb[l, n, m].cpu().numpy(), oeb[l, n, m], err_msg=f"block {b} slab")
+    return int(stats[0]), int(stats[3])
+
+
+def test_c5_matches_oracle_on_blocks(dev):
+    """BASELINE config 5 (41x41x3x16384, deep-bounce LUT, 82.6M rays) in one GPU launch; 1 % of
+    its 5043 FoV x wavelength blocks traced by the oracle."""
+    nblk = 41 * 41 * 3
+    sample = np.unique(np.linspace(0, nblk - 1, 51).astype(int))
+    bounces, replayed = _blocks_vs_oracle(dev, 41, 41, [0, 1, 2], 16384, sample, profile="deep")
+    assert bounces > 82_624_512
+    _record("C5_blocks_vs_oracle", {"blocks": len(sample), "gpu_bounces": bounces, "replayed": replayed})
+
+
+def test_main_default_job_matches_oracle_on_blocks(dev):
+    """The reference's default job (100x75 FoV x 3 lambda x 5000 rays, MAIN:16-17, 60-61) in one
+    GPU launch; 5 of its 22,500 blocks traced by the oracle."""
+    nblk = 100 * 75 * 3
+    sample = [0, 1, nblk // 3 + 1, 2 * nblk // 3 + 2, nblk - 1]
+    bounces, replayed = _blocks_vs_oracle(dev, 100, 75, [0, 1, 2], 5000, sample)
+    assert bounces > 112_500_000
+    _record("main_default_blocks_vs_oracle", {"blocks": len(sample), "gpu_bounces": bounces, "replayed": replayed})
