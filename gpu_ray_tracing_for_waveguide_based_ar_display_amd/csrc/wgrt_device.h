@@ -49,7 +49,7 @@ struct TraceArgs {
     const int32_t *order;   // Jones-vector variants: issue order of the 64-ray chunks (NULL: ascending)
     const double *jtiles;   // Jones-vector tiles (wgrt_common.h kJ*)
     int jtile_d;
-    // Jones-vector variants: out-couplings appended as (position, ray index) and binned into
+    // Jones-vector variants: out-couplings appended as (position, tile index) and binned into
     // matrix_EB by the epilogue kernel after the launch
     double2 *q_xy;
     uint32_t *q_i;
@@ -57,11 +57,11 @@ struct TraceArgs {
     double cert_tol;   // Jones-vector variants: base of the decision certification bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
-    // Jones-vector variants: per-wave counter partials {bounces, bad_rays, eyebox_hits, replayed}
-    // (trace-kernel waves first, then one slot per epilogue workgroup), summed into *stats by the
-    // epilogue's last workgroup -- no contended atomics on the four stats words
+    // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -}
+    // (trace-kernel workgroups first, then one slot per epilogue workgroup), summed into *stats by
+    // the epilogue's last workgroup -- no contended atomics on the four stats words
     unsigned long long *part;
-    int n_trace_waves;
+    int n_trace_waves;                  // partial slots of the trace kernel (one per workgroup)
     unsigned int *ticket;               // epilogue workgroups done (the last one sums and resets)
     unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
@@ -768,7 +768,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.mr = f.mr * rn;
     r.mi = f.mi * rn;
     const double ab = ba ? a0 : a1;
-    if (thr && t != 0.0) r.eerr += scl * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+    // ener accumulates every taken branch's relative error, the in-coupler states' too (no guard there,
+    // but their factors are part of ener at every later guard)
+    if (t != 0.0) r.eerr += scl * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
     r.x = ba ? xa : xb;

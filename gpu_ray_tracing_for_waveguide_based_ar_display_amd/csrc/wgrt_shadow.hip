@@ -208,7 +208,7 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
                 jr.mr = f.mr * rn;
                 jr.mi = f.mi * rn;
                 const double ab = b == 0 ? a0 : a1;
-                if (thr && t != 0.0) eerr += scl * JB[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+                if (t != 0.0) eerr += scl * JB[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
                 jener = jener * ab;
             }
         }

@@ -104,11 +104,11 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
     uint64_t h = 0, b = 0, bad = 0;
     for (unsigned long long j = tid; j < nq; j += nth) {
-        const uint32_t qi = A.q_i[j];
-        if (qi == 0xffffffffu) continue;   // a slot its wave left unused
-        const int64_t i = qi;
+        const uint32_t g = A.q_i[j];   // tile index (lambda * nx + m) * ny + n
         const double2 p = A.q_xy[j];
-        const int m = (int)A.m[i], n = (int)A.n[i], l = A.l ? (int)A.l[i] : 0;
+        if (g == 0xffffffffu) continue;   // a slot its wave left unused
+        const int n = (int)(g % (uint32_t)A.ny), m = (int)(g / (uint32_t)A.ny % (uint32_t)A.nx);
+        const int l = (int)(g / ((uint32_t)A.ny * (uint32_t)A.nx));
         h += eyebox_add(A, l, m, n, p.x, p.y);
     }
     for (unsigned long long k = tid; k < nr; k += nth) {
@@ -146,8 +146,9 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     __threadfence();   // acquire: every other workgroup's partials and the trace waves' (kernel boundary)
     const int nslots = A.n_trace_waves + (int)gridDim.x;
     uint64_t s0 = 0, s1 = 0, s2 = 0;
+#pragma unroll 4
     for (int k = threadIdx.x; k < nslots; k += blockDim.x) {
-        const volatile unsigned long long *slot = A.part + 4 * (size_t)k;
+        const unsigned long long *slot = A.part + 4 * (size_t)k;
         s0 += slot[0];
         s1 += slot[1];
         s2 += slot[2];
@@ -393,10 +394,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
                 nb = __shfl(nb, 0);
             }
-            if (out) {
+            if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
                 const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
                 KA(q_xy)[j] = double2{L.r.x, L.r.y};
-                KA(q_i)[j] = (uint32_t)L.i;
+                KA(q_i)[j] = (uint32_t)((L.T - KA(jtiles)) / A.jtile_d);
             }
             if (nout > rem) {
                 qbase = nb;
@@ -407,13 +408,19 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
-    // this wave's counters go to its partial slot (summed by the epilogue: no contended atomics)
+    // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
+    __shared__ unsigned long long red[4][2];
     tot_b = wave_sum(tot_b);
     tot_bad = wave_sum(tot_bad);
     if (lane == 0) {
-        unsigned long long *slot = KA(part) + 4 * ((size_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6));
-        slot[0] = tot_b;
-        slot[1] = tot_bad;
+        red[threadIdx.x >> 6][0] = tot_b;
+        red[threadIdx.x >> 6][1] = tot_bad;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        unsigned long long *slot = KA(part) + 4 * (size_t)blockIdx.x;
+        slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         slot[2] = 0;
         slot[3] = 0;
     }
@@ -637,8 +644,8 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
         if (e == hipSuccess) e = hipMemset(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long));
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
     }
-    // counter partials: one slot per trace-kernel wave (4 per workgroup) and per epilogue workgroup
-    const int64_t slots = grid * 4 + kEpilogueGroups;
+    // counter partials: one slot per trace-kernel workgroup and per epilogue workgroup
+    const int64_t slots = grid + kEpilogueGroups;
     if (sc->part_slots < slots) {
         HIP_TRY(hipStreamSynchronize(st));
         (void)hipFree(sc->part);
@@ -795,7 +802,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.ticket = (unsigned int *)(sc->ctr + (kHeads + 2) * kHeadStride);
     A.heads0 = sc->ctr;
     A.part = sc->part;
-    A.n_trace_waves = (int)grid * 4;
+    A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
     const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
     const dim3 g3((unsigned)grid), b3(256);
     if (variant == 9) {
