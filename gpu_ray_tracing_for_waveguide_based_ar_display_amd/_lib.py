@@ -18,7 +18,8 @@ LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
 ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
-            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_status_string",
+            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline",
+            "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
 
@@ -129,6 +130,8 @@ def load(path: str = LIB_PATH):
     L.wgrt_debug_shadow.restype = st
     L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp, _vp,
                                     _vp, _vp]
+    L.wgrt_debug_set_timeline.restype = None
+    L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
     L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
     L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
     L.wgrt_status_string.restype = ctypes.c_char_p

@@ -59,11 +59,12 @@ struct TraceArgs {
     uint32_t *replay_list;
     // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -}
     // (trace-kernel workgroups first, then one slot per epilogue workgroup), summed into *stats by
-    // the epilogue's last workgroup -- no contended atomics on the four stats words
+    // the finalize kernel -- no contended atomics on the four stats words
     unsigned long long *part;
     int n_trace_waves;                  // partial slots of the trace kernel (one per workgroup)
-    unsigned int *ticket;               // epilogue workgroups done (the last one sums and resets)
     unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
+    unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_set_timeline), NULL normally
+    int64_t timeline_waves;
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;

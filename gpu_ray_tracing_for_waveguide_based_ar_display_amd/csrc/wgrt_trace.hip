@@ -60,6 +60,8 @@ int g_jchunk = [] {
     return c >= 64 ? c / 64 * 64 : 64;
 }();
 double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
+unsigned long long *g_timeline = nullptr;   // wgrt_debug_set_timeline
+int64_t g_timeline_waves = 0;
 
 
 #define HIP_TRY(expr)                                                                       \
@@ -78,27 +80,24 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 }
 
 // Launch scratch counters of the Jones-vector variants: kHeads work-queue heads, then the replay
-// count, the out-coupling queue count and the epilogue ticket, each on its own 128-B line.
+// count and the out-coupling queue count, each on its own 128-B line.
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
-constexpr int kScratchCtr = (kHeads + 3) * kHeadStride;   // heads, replay count, queue count, ticket
+constexpr int kScratchCtr = (kHeads + 2) * kHeadStride;   // heads, replay count, queue count
 constexpr int kScratchCtrWords = kScratchCtr;
 
-// Runs right behind every Jones-vector launch on its stream (one launch instead of three):
-//  1. bins the queued out-couplings (entry j: position q_xy[j] of ray q_i[j]) into matrix_EB --
-//     the eyebox predicate, its divisions and the atomics stay out of the bounce loop; cells
-//     count hits (+1.0f), so the binning order does not matter;
+// Runs right behind every Jones-vector launch on its stream:
+//  1. bins the queued out-couplings (entry j: position q_xy[j], tile index q_i[j]) into
+//     matrix_EB -- the eyebox predicate, its divisions and the atomics stay out of the bounce
+//     loop; cells count hits (+1.0f), so the binning order does not matter;
 //  2. re-traces the rays the launch abandoned (uncertain decisions; nothing of them was written)
 //     from their launch-start state with the reference arithmetic (usually none);
-//  3. its last workgroup (ticket) sums the per-wave counter partials of the trace kernel and of
-//     the epilogue workgroups into *stats -- four atomics per launch -- and zeroes the launch
-//     scratch counters (queue heads, replay / queue counts, ticket) for the next launch on the
-//     stream, which therefore needs no memset of its own.
+//  3. stores its workgroup's counters in its partial slot (plain stores: finalize_kernel, the
+//     next kernel on the stream, sums them -- no contended atomics, no device-scope fences).
 constexpr int kEpilogueGroups = 256;
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
-    __shared__ unsigned long long red[4][4];
-    __shared__ bool last;
+    __shared__ unsigned long long red[4][3];
     const unsigned long long nq = *A.q_count, nr = *A.replay_count;
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
@@ -122,11 +121,11 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
             A.rng[i] = st;
         }
     }
-    const int w = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const int w = threadIdx.x >> 6;
     b = wave_sum(b);
     bad = wave_sum(bad);
     h = wave_sum(h);
-    if (lane == 0) {
+    if ((threadIdx.x & 63) == 0) {
         red[w][0] = b;
         red[w][1] = bad;
         red[w][2] = h;
@@ -138,13 +137,17 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
         slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
         slot[3] = 0;
-        __threadfence();   // partials visible device-wide before the ticket
-        last = atomicAdd(A.ticket, 1u) == gridDim.x - 1;
     }
-    __syncthreads();
-    if (!last) return;
-    __threadfence();   // acquire: every other workgroup's partials and the trace waves' (kernel boundary)
-    const int nslots = A.n_trace_waves + (int)gridDim.x;
+}
+
+// One workgroup after the epilogue: sums the partial slots of the trace kernel's and the
+// epilogue's workgroups into *stats (four atomics per launch) and zeroes the launch scratch
+// counters (queue heads, replay / queue counts) for the next launch on the stream, which
+// therefore needs no memset of its own.
+__global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilogue) {
+    __shared__ unsigned long long red[4][3];
+    const unsigned long long nr = *A.replay_count;
+    const int nslots = A.n_trace_waves + n_epilogue;
     uint64_t s0 = 0, s1 = 0, s2 = 0;
 #pragma unroll 4
     for (int k = threadIdx.x; k < nslots; k += blockDim.x) {
@@ -156,26 +159,23 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     s0 = wave_sum(s0);
     s1 = wave_sum(s1);
     s2 = wave_sum(s2);
-    __syncthreads();
-    if (lane == 0) {
+    const int w = threadIdx.x >> 6;
+    if ((threadIdx.x & 63) == 0) {
         red[w][0] = s0;
         red[w][1] = s1;
         red[w][2] = s2;
     }
-    __syncthreads();
-    if (threadIdx.x == 0) {
+    __syncthreads();   // every thread has read the counts it needs before they are zeroed
+    if (threadIdx.x == 0 && A.stats) {
         wgrt_trace_stats *st = A.stats;
-        if (st) {
-            const unsigned long long t0 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-            const unsigned long long t1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-            const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
-            if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
-            if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
-            if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
-            if (nr) atomicAdd((unsigned long long *)&st->replayed, nr);
-        }
+        const unsigned long long t0 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        const unsigned long long t1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
+        if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
+        if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
+        if (nr) atomicAdd((unsigned long long *)&st->replayed, nr);
     }
-    // zero the launch scratch counters for the next launch on this stream
     if (threadIdx.x < kScratchCtrWords) A.heads0[threadIdx.x] = 0ull;
 }
 
@@ -224,6 +224,13 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     int pend_h = -1;                  // head of the dequeue in flight (-1: none)
     unsigned long long pend_v = 0;    // its result (lane 0)
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
+    // debug timeline (wgrt_debug_set_timeline; NULL in production): per wave, start / queue
+    // exhausted / end (s_memrealtime, 100 MHz), passes, and lane-passes with a ray in flight
+    unsigned long long *const tl = KA(timeline);
+    const int64_t tl_wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
+    const bool tl_on = tl != nullptr && tl_wave < KA(timeline_waves);
+    unsigned long long tl_passes = 0, tl_lanes = 0;
+    if (tl_on && lane == 0) tl[6 * tl_wave] = __builtin_amdgcn_s_memrealtime();
     uint32_t cur_k = 0;               // the item's iteration
     bool exhausted = false;
     bool active = false, waiting = false;
@@ -337,6 +344,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 pend_h = -1;
                 if (!got) {
                     exhausted = true;
+                    if (tl_on && lane == 0) tl[6 * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
                     break;
                 }
                 pend_h = head;   // issue the next dequeue now; read when this item runs dry
@@ -363,6 +371,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             need = __ballot(!active && !waiting);
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
+        if (tl_on) {
+            ++tl_passes;
+            tl_lanes += __popcll(__ballot(active));
+        }
         bool out = false;
         if (active && blk >= 0) {
             const int next = interact(A, loc, L, blk, kind, entry);
@@ -408,6 +420,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
+    if (tl_on && lane == 0) {
+        tl[6 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
+        tl[6 * tl_wave + 3] = tl_passes;
+        tl[6 * tl_wave + 4] = tl_lanes;
+        tl[6 * tl_wave + 5] = (unsigned long long)xcc_id();
+    }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
     __shared__ unsigned long long red[4][2];
     tot_b = wave_sum(tot_b);
@@ -768,6 +786,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
     A.cert_tol = g_cert_tol;
+    A.timeline = g_timeline;
+    A.timeline_waves = g_timeline_waves;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
     A.n_iter = 1;
@@ -799,7 +819,6 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.q_xy = sc->q_xy;
     A.q_i = sc->q_i;
     A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
-    A.ticket = (unsigned int *)(sc->ctr + (kHeads + 2) * kHeadStride);
     A.heads0 = sc->ctr;
     A.part = sc->part;
     A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
@@ -819,6 +838,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     }
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, A, kEpilogueGroups);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }
@@ -970,6 +991,11 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
         out_mask[i] = mask;
     }
     return WGRT_OK;
+}
+
+void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves) {
+    g_timeline = n_waves > 0 ? buf : nullptr;
+    g_timeline_waves = n_waves > 0 ? n_waves : 0;
 }
 
 double wgrt_debug_set_cert_tol(double cert_tol) {

@@ -256,6 +256,12 @@ wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, in
                               int single, uint32_t *rng_states, uint32_t *per_ray_bounces, wgrt_shadow_stats *stats,
                               void *stream);
 
+/* Debug hook (process-wide): while set, every Jones-vector launch records, per wave w < n_waves
+ * of its grid, 6 words into the DEVICE buffer buf[6 w ..]: start, queue-exhausted and end times
+ * (s_memrealtime, 100 MHz), passes of the wave loop, lane-passes with a ray in flight, XCD id.
+ * buf = NULL or n_waves = 0 turns it off (the default). */
+void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves);
+
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */
 wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, double *out, void *stream);

@@ -37,10 +37,4 @@ if [[ $STEPS == *traffic* ]]; then
   timeout -k 10 900 python tools/pmc_traffic.py "$OUT/${TAG}_traffic.json" ${BENCH_ARGS:-} > "$OUT/${TAG}_traffic.log" 2>&1
   ok_or_stop $? traffic
 fi
-if [[ $STEPS == *pcsamp* ]]; then
-  (cd /tmp && timeout -k 10 300 rocprofv3 --pc-sampling-beta-enabled --pc-sampling-method ${PCS_METHOD:-stochastic} \
-    --pc-sampling-unit ${PCS_UNIT:-cycles} --pc-sampling-interval ${PCS_INTERVAL:-65536} -d "$OUT/${TAG}_pcs" -o run \
-    --output-format csv -- python3 "$ROOT/bench.py" --no-cpu-baseline --no-extras --steps 10 > "$OUT/${TAG}_pcs.log" 2>&1)
-  ok_or_stop $? pcsamp
-fi
 exit 0

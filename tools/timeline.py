@@ -1,0 +1,83 @@
+#!/usr/bin/env python3
+"""Wave timeline of one Jones-vector launch (wgrt_debug_set_timeline): where a launch's time goes.
+
+Runs the bench workload (C3 by default), records per wave: start, queue-exhausted and end
+times, passes and lane-passes, and prints a summary: launch span, when the work queue ran dry,
+the drain (tail) after it, lane occupancy before and after, per-XCD end times.
+Usage: python tools/timeline.py [--config C3] [--num-iter 1] [--variant 0] [--out FILE]
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, REPO)
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--num-iter", type=int, default=1)
+    ap.add_argument("--variant", type=int, default=0)
+    ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--out", default=None)
+    a = ap.parse_args()
+    import torch
+    import bench
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, trace_fullcolor
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+
+    dev = torch.device("cuda", 0)
+    cfg = bench.CONFIGS[a.config]
+    nx, ny, lam, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
+    geom = design_geometry(nx, ny)
+    luts = synthetic_luts(geom, seed=0, profile=cfg["profile"])
+    pts = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
+    scene = Scene.from_geometry(geom, luts)
+    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(0, nx * ny * len(lam))
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    nw = 256 * 8 * 4 * 2
+    buf = torch.zeros(6 * nw, dtype=torch.int64, device=dev)
+    L = _lib.load()
+    for _ in range(2):
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter)
+    res = []
+    for rep in range(a.reps):
+        buf.zero_()
+        L.wgrt_debug_set_timeline(ctypes.c_void_p(buf.data_ptr()), nw)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter)
+        e1.record()
+        torch.cuda.synchronize()
+        L.wgrt_debug_set_timeline(None, 0)
+        t = buf.cpu().numpy().reshape(-1, 6)
+        t = t[t[:, 0] > 0]
+        start, exh, end, passes, lanes, xcc = (t[:, k].astype(np.float64) for k in range(6))
+        t0 = start.min()
+        us = lambda v: (v - t0) / 100.0   # 100 MHz ticks -> us
+        r = {"event_ms": e0.elapsed_time(e1), "waves": int(len(t)),
+             "start_us": [float(np.percentile(us(start), q)) for q in (0, 50, 100)],
+             "exhausted_us": [float(np.percentile(us(exh), q)) for q in (0, 10, 50, 90, 100)],
+             "end_us": [float(np.percentile(us(end), q)) for q in (0, 10, 50, 90, 99, 100)],
+             "passes_per_wave": [float(np.percentile(passes, q)) for q in (0, 50, 100)],
+             "mean_active_lanes_per_pass": float(lanes.sum() / max(passes.sum(), 1)),
+             "end_by_xcd_us": {int(x): float(us(end[xcc == x]).max()) for x in np.unique(xcc)},
+             "exhausted_by_xcd_us": {int(x): float(us(exh[xcc == x]).max()) for x in np.unique(xcc)}}
+        res.append(r)
+        print(json.dumps(r), flush=True)
+    if a.out:
+        with open(a.out, "w") as f:
+            json.dump({"config": a.config, "num_iter": a.num_iter, "runs": res}, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
