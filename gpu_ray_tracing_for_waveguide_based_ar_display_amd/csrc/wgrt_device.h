@@ -65,6 +65,7 @@ struct TraceArgs {
     unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
     unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_set_timeline), NULL normally
     int64_t timeline_waves;
+    int drain_hops;                     // miss hops per pass once the work queue is exhausted
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;
@@ -795,10 +796,10 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 // fused).
 constexpr int kJMaxHops = 1;
 template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind, int max_hops = kJMaxHops) {
     JRay &r = L.r;
     for (int hops = 0;; ++hops) {
-        if (hops >= kJMaxHops) return kTransit;
+        if (hops >= max_hops) return kTransit;
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
         const auto c = (typename Loc::Word)L.pf;

@@ -61,6 +61,11 @@ int g_jchunk = [] {
 }();
 double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
 unsigned long long *g_timeline = nullptr;   // wgrt_debug_set_timeline
+// miss hops a lane may take per pass once the work queue is exhausted (env WGRT_DRAIN_HOPS)
+int g_drain_hops = [] {
+    const char *v = getenv("WGRT_DRAIN_HOPS");
+    return v ? atoi(v) : 1;
+}();
 int64_t g_timeline_waves = 0;
 
 
@@ -294,7 +299,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
     for (;;) {
         if (active) {
-            blk = advance(A, loc, L, kind);
+            // once the queue has run dry a lane may take several miss hops per pass (g_drain_hops): the
+            // wave's interaction step no longer competes with refills, and a drain-phase ray's
+            // chain of passes is the launch's critical path
+            blk = (exhausted && A.drain_hops > 1) ? advance(A, loc, L, kind, A.drain_hops) : advance(A, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
@@ -787,6 +795,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.inv_n_g = 1.0 / s->n_g;
     A.cert_tol = g_cert_tol;
     A.timeline = g_timeline;
+    A.drain_hops = g_drain_hops;
     A.timeline_waves = g_timeline_waves;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;

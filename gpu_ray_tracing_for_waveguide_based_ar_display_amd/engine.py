@@ -136,14 +136,16 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
         "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
 
 
-def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None):
-    """Issue order of the 64-ray chunks for ``chunk_order``: chunks whose rays belong to the
-    (wavelength, FoV) tiles with the longest mean lifetime in a previous launch go first, so
-    the rays that outlive the work queue come from short-lived tiles and the launch's
-    straggler tail shortens.  ``per_ray_bounces`` from an earlier launch of the same batch
-    (``trace_*(per_ray_bounces=...)``), ``tile_of_ray`` any integer tile key per ray (e.g.
-    ``(lmd_num * NX + m) * NY + n``).  Device tensors in, int32 device permutation out
-    (a few small torch ops, no host sync).  A pure scheduling hint: results are unchanged."""
+def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None, heads: int = 8):
+    """Issue order of the 64-ray chunks for ``chunk_order``: within each of the kernel's per-XCD
+    work-queue segments (chunk positions [c * x / heads, c * (x + 1) / heads), include/wgrt.h), the
+    chunks whose rays belong to the (wavelength, FoV) tiles with the longest mean lifetime in a
+    previous launch go first, so the rays that outlive the work queue come from short-lived
+    tiles and the launch's straggler tail shortens; each segment keeps its own chunks (and the
+    tiles they read stay in that XCD's L2).  ``per_ray_bounces`` from an earlier launch of the
+    same batch (``trace_*(per_ray_bounces=...)``), ``tile_of_ray`` any integer tile key per ray
+    (e.g. ``(lmd_num * NX + m) * NY + n``).  Device tensors in, int32 device permutation out (a
+    few small torch ops, no host sync).  A pure scheduling hint: results are unchanged."""
     b = per_ray_bounces.to(torch.float32)
     key = tile_of_ray.to(torch.int64)
     nt = int(n_tiles) if n_tiles is not None else int(key.max().item()) + 1
@@ -153,7 +155,11 @@ def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = Non
     N = b.numel()
     first = torch.arange(0, N, CHUNK, device=b.device)
     chunk_key = mean[key[first]]
-    return torch.argsort(chunk_key, descending=True, stable=True).to(torch.int32)
+    n = chunk_key.numel()
+    seg = torch.arange(n, device=b.device) * heads // n     # segment of each chunk position
+    # sort by (segment asc, lifetime desc): lifetimes are bounded, so one composite key does it
+    comp = seg.to(torch.float64) * 1e9 - chunk_key.to(torch.float64)
+    return torch.argsort(comp, stable=True).to(torch.int32)
 
 
 def init_rays(points, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int, blocks=None,

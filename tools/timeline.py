@@ -25,13 +25,15 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--order", default="none", choices=["none", "lifetime"],
+                    help="chunk issue order: ascending, or long-lived tiles first (from a previous launch)")
     a = ap.parse_args()
     import torch
     import bench
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, trace_fullcolor
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, schedule_by_lifetime, trace_fullcolor
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
 
@@ -47,15 +49,22 @@ def main():
     nw = 256 * 8 * 4 * 2
     buf = torch.zeros(6 * nw, dtype=torch.int64, device=dev)
     L = _lib.load()
+    order = None
+    if a.order == "lifetime":
+        per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, per_ray_bounces=per)
+        tile = ((rays["lmd_num"].long() * nx + rays["m"].long()) * ny + rays["n"].long())
+        order = schedule_by_lifetime(per, tile, len(lam) * nx * ny)
+    kw = dict(chunk_order=order) if order is not None else {}
     for _ in range(2):
-        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter)
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter, **kw)
     res = []
     for rep in range(a.reps):
         buf.zero_()
         L.wgrt_debug_set_timeline(ctypes.c_void_p(buf.data_ptr()), nw)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter)
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter, **kw)
         e1.record()
         torch.cuda.synchronize()
         L.wgrt_debug_set_timeline(None, 0)
@@ -72,6 +81,8 @@ def main():
              "mean_active_lanes_per_pass": float(lanes.sum() / max(passes.sum(), 1)),
              "end_by_xcd_us": {int(x): float(us(end[xcc == x]).max()) for x in np.unique(xcc)},
              "exhausted_by_xcd_us": {int(x): float(us(exh[xcc == x]).max()) for x in np.unique(xcc)}}
+        r["order"] = a.order
+        r["drain_hops"] = int(os.environ.get("WGRT_DRAIN_HOPS", "1"))
         res.append(r)
         print(json.dumps(r), flush=True)
     if a.out:
