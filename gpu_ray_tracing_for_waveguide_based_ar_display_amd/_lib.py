@@ -18,7 +18,7 @@ LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
 ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
-            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline",
+            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline", "wgrt_debug_set_cert_tol32",
             "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -68,7 +68,8 @@ class LaunchOpts(ctypes.Structure):
 
 class ShadowStats(ctypes.Structure):
     _fields_ = [("decisions", ctypes.c_uint64), ("uncertain", ctypes.c_uint64), ("silent_flips", ctypes.c_uint64),
-                ("bounces", ctypes.c_uint64), ("max_ratio", ctypes.c_double),
+                ("bounces", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64), ("max_ratio", ctypes.c_double),
+                ("max_ratio32", ctypes.c_double),
                 ("max_ratio_by_depth", ctypes.c_double * 6), ("decisions_by_depth", ctypes.c_uint64 * 6),
                 ("ratio_hist", ctypes.c_uint64 * 20), ("max_ener_ratio", ctypes.c_double)]
 
@@ -132,6 +133,8 @@ def load(path: str = LIB_PATH):
                                     _vp, _vp]
     L.wgrt_debug_set_timeline.restype = None
     L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
+    L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
+    L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]
     L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
     L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
     L.wgrt_status_string.restype = ctypes.c_char_p

@@ -64,15 +64,17 @@ constexpr int kJHop = 8;          // (cos, sin) of 2 lut_TIR[0] (R2 miss hop), o
 constexpr int kJCosIc1 = 12;      // cos(lut_ic1[l, m, n, 0].real)
 constexpr int kJGrowth = 13;      // max(1, max_k |lut_TIR[k]| / pi): bounds the reference's unwrapped phase growth
 constexpr int kJHeader = 16;
-constexpr int kJBlock = 32;       // cosA[3], Wsum, rec[3][8], W[3], pad
+constexpr int kJBlock = 48;       // cosA[3], Wsum, rec32[3][8] (floats), rec[3][8], W[3], pad
 constexpr int kJBlockCos = 0;
 constexpr int kJBlockWsum = 3;    // sum of W[k]
-constexpr int kJBlockRec = 4;
+constexpr int kJBlockRec32 = 4;   // the three matrices rounded to float (96 B): the estimate's input
+constexpr int kJBlockRec = 16;    // the three matrices in double precision
 // W[k] = ((|p|+|r|)^2 + (|q|+|s|)^2) * |cosA_k| * f_k (f_k the n_g factor of the branch): for a
 // field state E, |M_k E|^2 * cosA_k * f_k is computed to within D * W[k] * |E|^2 by any two
-// evaluations whose states agree to within D / 4 (relative) -- the bound the Jones-vector
-// variants certify their Monte-Carlo decisions against.
-constexpr int kJBlockW = 28;
+// evaluations whose states and matrices agree to within D / 4 (relative) -- the bound the
+// Jones-vector variants certify their Monte-Carlo decisions against (D = cert_tol for the
+// double-precision evaluation, cert_tol32 for the single-precision estimate).
+constexpr int kJBlockW = 40;
 WGRT_HD int jtile_doubles(int nfc, int noc) { return kJHeader + kJBlock * (3 + 2 * nfc + 2 * noc); }
 
 // block index: 0 in-coupling, 1 R0, 2 R1, 3 + k R2 slice k, 3 + nfc + k R3,

@@ -54,7 +54,8 @@ struct TraceArgs {
     double2 *q_xy;
     uint32_t *q_i;
     unsigned long long *q_count;
-    double cert_tol;   // Jones-vector variants: base of the decision certification bound
+    double cert_tol;   // Jones-vector variants: base of the double-precision certification bound
+    double cert_tol32; // ... and of the single-precision estimate's bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
     // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -}
@@ -580,8 +581,17 @@ struct JLane {
     uint32_t bounces;
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
-    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
+    // locator cell word of (x, y), loaded a step ahead: an interaction loads the words of both
+    // candidate positions and keeps both, the choice is resolved where the word is used (next
+    // pass), so the interaction never waits for those loads
+    uint64_t pfa, pfb;
+    bool pfsel;              // true: pfa
 };
+
+// Regions 6 / 7: an in-coupler state's branch was taken and the in-coupler test at the new
+// position (GRTF:883-900, 928-949, 974-995) is still to be made -- at the next pass, on the
+// prefetched cell word: 6 -> R0 if inside the IC else R2; 7 -> R1 if inside, else the ray dies.
+constexpr int kRegionIcA = 6, kRegionIcB = 7;
 
 enum : int { kUncertain = -3, kOut = -4 };
 
@@ -622,7 +632,8 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.s = rs;
     L.r.region = 0;
     L.bounces = 1;
-    L.pf = 0ull;
+    L.pfa = L.pfb = 0ull;
+    L.pfsel = true;
     return ok;
 }
 
@@ -679,9 +690,107 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
     return L.cells[iy * L.ncx + ix];
 }
 
+// One interaction block's single-precision copy of its Jones matrices (p, q, r, s per branch).
+struct Rec32 {
+    float pr, pi, qr, qi, rr, ri, sr, si;
+};
+
+__device__ __forceinline__ Rec32 load_rec32(const float *p) {
+    const float4 a = *(const float4 *)p, b = *(const float4 *)(p + 4);
+    return Rec32{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
+}
+
+// |M E|^2 in single precision (the certified estimate of a branch efficiency's numerator).
+__device__ __forceinline__ float norm2_32(const Rec32 &c, float er, float ei, float mr, float mi) {
+    const float yr = fmaf(c.pr, er, fmaf(-c.pi, ei, fmaf(c.rr, mr, -c.ri * mi)));
+    const float yi = fmaf(c.pr, ei, fmaf(c.pi, er, fmaf(c.rr, mi, c.ri * mr)));
+    const float zr = fmaf(c.qr, er, fmaf(-c.qi, ei, fmaf(c.sr, mr, -c.si * mi)));
+    const float zi = fmaf(c.qr, ei, fmaf(c.qi, er, fmaf(c.sr, mi, c.si * mr)));
+    return fmaf(yr, yr, fmaf(yi, yi, fmaf(zr, zr, zi * zi)));
+}
+
+// A Monte-Carlo decision of the Jones-vector lane: the branch efficiencies a_k (estimates of the
+// reference's e_k), the draw u, and whether the decision is certified at bound scale `scl`
+// (tol = scl * sum_k W[k]; the single-wavelength guard margins use scl * W[k]).
+struct JDecision {
+    double a0, a1, a2;
+    bool ok, s0, s1, s2;
+};
+
+__device__ __forceinline__ void jones_decide(JDecision &d, double u, double scl, const double *B, double Wsum,
+                                             bool three, bool thr, double t, double ener, double eerr) {
+    const double c0 = d.a0, c1 = d.a0 + d.a1, c2 = c1 + d.a2;
+    const double tol = scl * Wsum;
+    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic.
+    // Non-short-circuit (&, |) throughout: one straight-line evaluation per lane.
+    bool ok = (tol > 1e-250) & (fabs(u - c0) > tol) & (fabs(u - c1) > tol) & (!three | (fabs(u - c2) > tol));
+    bool p0 = true, p1 = true, p2 = true;
+    if (t == 0.0) {   // full colour (uniform branch)
+        // a branch the certified draw selects has e_k > tol (it lies between two thresholds more
+        // than tol from the draw), so ener * e_k > 0 holds for the reference too unless that
+        // product could underflow
+        ok = ok & (!thr | (ener * tol > 1e-290));
+    } else if (thr) {
+        // ener * e_k > threshold (GRTF:606): certified with ener's tracked relative error
+        const double g0 = ener * d.a0, g1 = ener * d.a1, g2 = ener * d.a2;
+        const double re = eerr + 1e-15;
+        const double m0 = re * fabs(g0) + ener * scl * B[kJBlockW] * 1.01;
+        const double m1 = re * fabs(g1) + ener * scl * B[kJBlockW + 1] * 1.01;
+        const double m2 = re * fabs(g2) + ener * scl * B[kJBlockW + 2] * 1.01;
+        p0 = g0 > t;
+        p1 = g1 > t;
+        p2 = g2 > t;
+        ok = ok & ((u > c0) | (fabs(g0 - t) > m0)) & ((u > c1) | (fabs(g1 - t) > m1)) &
+             (!three | (u > c2) | (fabs(g2 - t) > m2));
+    }
+    d.s0 = (u <= c0) & p0;
+    d.s1 = !d.s0 & (u <= c1) & p1;
+    d.s2 = !d.s0 & !d.s1 & three & (u <= c2) & p2;   // out-coupling (GRTF:1162-1171, 1231-1240)
+    d.ok = ok;
+}
+
+// The efficiencies from the single-precision matrices (the estimate every decision starts with).
+__device__ __forceinline__ void estimate32(JDecision &d, const double *B, const JRay &r, bool three, double inv,
+                                           double f01, double inv_n_g, const double4 &cw) {
+    const float *R = (const float *)(B + kJBlockRec32);
+    const Rec32 k0 = load_rec32(R), k1 = load_rec32(R + 8);
+    const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
+    const double q0 = (double)norm2_32(k0, er, ei, mr, mi), q1 = (double)norm2_32(k1, er, ei, mr, mi);
+    double q2 = 0.0;
+    if (three) q2 = (double)norm2_32(load_rec32(R + 16), er, ei, mr, mi);
+    d.a0 = q0 * cw.x * inv * f01;
+    d.a1 = q1 * cw.y * inv * f01;
+    d.a2 = three ? q2 * cw.z * inv * inv_n_g : 0.0;
+}
+
+// The same in double precision, one matrix at a time (the rare re-evaluation of a decision the
+// single-precision estimate could not certify; register-light rather than fast).
+__device__ __forceinline__ void estimate64(JDecision &d, const double *B, const JRay &r, bool three, double inv,
+                                           double f01, double inv_n_g, const double4 &cw) {
+    double q[3] = {0.0, 0.0, 0.0};
+#pragma unroll 1
+    for (int k = 0; k < (three ? 3 : 2); ++k) {
+        const double v = norm2(jones(load_rec(B + kJBlockRec + 8 * k), r));
+        q[0] = k == 0 ? v : q[0];
+        q[1] = k == 1 ? v : q[1];
+        q[2] = k == 2 ? v : q[2];
+    }
+    d.a0 = q[0] * cw.x * inv * f01;
+    d.a1 = q[1] * cw.y * inv * f01;
+    d.a2 = three ? q[2] * cw.z * inv * inv_n_g : 0.0;
+}
+
 // Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
 // kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
 // of it has been written) and replayed.
+//
+// A decision is first taken from single-precision efficiencies, certified against the bound
+// scaled by A.cert_tol32 (which covers single-precision rounding of |M E|^2 with a wide margin,
+// wgrt_shadow.hip measures it); the rare decision that bound leaves open is re-evaluated in
+// double precision against the A.cert_tol bound, and only if that fails too is the ray
+// abandoned.  The taken branch's field is always computed in double precision from its
+// double-precision matrix (loaded after the decision), so the carried Jones vector and ener
+// are the same values the all-double evaluation gives.
 template <class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
                                         bool entry) {
@@ -698,9 +807,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
     const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
-    const Rec k0 = load_rec(B + kJBlockRec), k1 = load_rec(B + kJBlockRec + 8);
-    Rec k2{};
-    if (three) k2 = load_rec(B + kJBlockRec + 16);
     const double xa = r.x + mva.x, ya = r.y + mva.y;
     const double xb = r.x + mvb.x, yb = r.y + mvb.y;
     const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
@@ -714,95 +820,72 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.hops = 0;
     const double denom = entry ? cg.x : r.cos_t;
     const double u = rng_draw(r.s, A.gid_offset + L.i);
-    const JField f0 = jones(k0, r), f1 = jones(k1, r);
-    const double q0 = norm2(f0), q1 = norm2(f1);
-    const double q2 = three ? norm2(jones(k2, r)) : 0.0;
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
-    const double a0 = q0 * cw.x * inv * f01, a1 = q1 * cw.y * inv * f01;
-    const double a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
-    const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double scl = A.cert_tol * fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
-    const double tol = scl * cw.w;
-    // NaN anywhere fails these comparisons: such a ray is replayed by the reference arithmetic.
-    // Non-short-circuit (&, |) throughout: one straight-line evaluation per lane.
-    bool ok = (tol > 1e-250) & (fabs(u - c0) > tol) & (fabs(u - c1) > tol) & (!three | (fabs(u - c2) > tol));
+    const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
     const double t = A.threshold;
-    bool p0 = true, p1 = true, p2 = true;
-    if (t == 0.0) {   // full colour (uniform branch)
-        // a branch the certified draw selects has e_k > tol (it lies between two thresholds more
-        // than tol from the draw), so ener * e_k > 0 holds for the reference too unless that
-        // product could underflow
-        ok = ok & (!thr | (r.ener * tol > 1e-290));
-    } else if (thr) {
-        {
-            // ener * e_k > threshold (GRTF:606): certified with ener's tracked relative error
-            const double g0 = r.ener * a0, g1 = r.ener * a1, g2 = r.ener * a2;
-            const double re = r.eerr + 1e-15;
-            const double m0 = re * fabs(g0) + r.ener * scl * B[kJBlockW] * 1.01;
-            const double m1 = re * fabs(g1) + r.ener * scl * B[kJBlockW + 1] * 1.01;
-            const double m2 = re * fabs(g2) + r.ener * scl * B[kJBlockW + 2] * 1.01;
-            p0 = g0 > t;
-            p1 = g1 > t;
-            p2 = g2 > t;
-            ok = ok && (u > c0 || fabs(g0 - t) > m0) && (u > c1 || fabs(g1 - t) > m1) &&
-                 (!three || u > c2 || fabs(g2 - t) > m2);
-        }
+    JDecision d;
+    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
+    jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, r.eerr);
+    if (!d.ok) {   // rare: the double-precision evaluation
+        estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
+        jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, r.eerr);
     }
-    const bool s0 = (u <= c0) & p0;
-    const bool s1 = !s0 & (u <= c1) & p1;
-    const bool s2 = !s0 & !s1 & three & (u <= c2) & p2;   // out-coupling (GRTF:1162-1171, 1231-1240)
-    const bool ba = s0;
-    const JField f = ba ? f0 : f1;
-    const double n2 = ba ? q0 : q1;
-    ok = ok & (!(s0 | s1) | (n2 > 1e-300));
     // one exit for every outcome but a taken branch; an out-coupling is appended to the
     // out-coupling queue by the caller (at (r.x, r.y))
-    const int code = !ok ? kUncertain : s2 ? kOut : !(s0 | s1) ? kDie : 0;
+    const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
     if (code != 0) return code;
+    const bool ba = d.s0;
     const int b = ba ? 0 : 1;
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
+    const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
+    const double n2 = norm2(f);
+    if (!(n2 > 1e-300)) return kUncertain;
     const double rn = rsq_nr(n2);
     r.er = f.er * rn;
     r.ei = f.ei * rn;
     r.mr = f.mr * rn;
     r.mi = f.mi * rn;
-    const double ab = ba ? a0 : a1;
+    const double ab = n2 * (ba ? cw.x : cw.y) * inv * f01;   // the taken branch's efficiency, double precision
     // ener accumulates every taken branch's relative error, the in-coupler states' too (no guard there,
     // but their factors are part of ener at every later guard)
-    if (t != 0.0) r.eerr += scl * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+    if (t != 0.0) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
     r.x = ba ? xa : xb;
     r.y = ba ? ya : yb;
     r.gx = ba ? mva.x : mvb.x;
     r.gy = ba ? mva.y : mvb.y;
-    L.pf = ba ? pa : pb;
-    if (kind == 0) {
-        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
-        if (ba) return in_ic ? 0 : 2;
-        return in_ic ? 1 : kDie;
-    }
+    L.pfa = pa;
+    L.pfb = pb;
+    L.pfsel = ba;
+    if (kind == 0) return ba ? kRegionIcA : kRegionIcB;   // in-coupler test at the next pass
     if (kind <= 2) return ba ? 2 : 3;
     return ba ? 4 : 5;
 }
 
 // Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
 // that need no Monte-Carlo interaction, at most kJMaxHops per call: every iteration then tests
-// a cell word loaded a pass earlier, L.pf, and a hop issues the load of the next one.  1 measured
+// a cell word loaded a pass earlier (JLane::pfa / pfb), and a hop issues the load of the next one.  1 measured
 // best on C3 (2 and 4 slower); a compile-time bound, not a kernarg, straightens the loop (-2 %
 // fused).
 constexpr int kJMaxHops = 1;
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind, int max_hops = kJMaxHops) {
     JRay &r = L.r;
+    auto c = (typename Loc::Word)(L.pfsel ? L.pfa : L.pfb);
+    if (r.region >= kRegionIcA) {   // the pending in-coupler test of the last interaction
+        const bool in_ic = in_poly_w<true>(loc, c, kPolyIC, r.x, r.y);
+        if (r.region == kRegionIcA) r.region = in_ic ? 0 : 2;
+        else if (in_ic) r.region = 1;
+        else return kDie;   // GRTF:899-900, 948-949, 994-995
+    }
     for (int hops = 0;; ++hops) {
         if (hops >= max_hops) return kTransit;
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
-        const auto c = (typename Loc::Word)L.pf;
         if (!in_poly_w<true>(loc, c, kPolyEff1, r.x, r.y)) return kDie;
         const int region = r.region;
         if (region <= 1) {
@@ -826,7 +909,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         r.x = r.x + r.gx;
         r.y = r.y + r.gy;
         ++r.hops;
-        L.pf = locate_c(loc, r.x, r.y);   // used from the next pass on
+        c = locate_c(loc, r.x, r.y);   // used from the next pass on (or the next hop of this call)
+        L.pfa = c;
+        L.pfsel = true;
     }
 }
 

@@ -370,6 +370,8 @@ void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std
                 }
                 O[kJBlockW + k] = w;
                 sum += w;
+                float *r32 = (float *)(O + kJBlockRec32) + 8 * k;   // the estimate's single-precision copy
+                for (int j = 0; j < 8; ++j) r32[j] = (float)rec[j];
             }
             O[kJBlockWsum] = sum * 1.01;
         }

@@ -16,11 +16,14 @@
 // Alongside, the lane carries the Jones-vector state exactly as the product lane does (the
 // block's Jones matrices with the TIR step folded in, miss-hop phase steps applied as a power at
 // the next interaction, rsq normalisation) and, at every decision, evaluates the product lane's
-// thresholds c_k^J and its bound tol.  It records
+// thresholds c_k^J and its bounds tol -- for its single-precision estimate (tol32, the bound
+// every decision is first certified against) and its double-precision re-evaluation (tol64).
+// It records
 //     ratio = max_k |c_k^J - c_k^ref| / tol
-// (max overall, by bounce depth, and as a log10 histogram), the decisions the product lane
-// would leave uncertain (replayed), and "silent flips": decisions the product lane would
-// certify although they differ from the reference's -- which must never happen.  The ray always
+// for both (max overall; for tol32 also by bounce depth and as a log10 histogram), the decisions
+// the single-precision estimate leaves to the double-precision one (fallbacks), the decisions
+// the product lane would leave uncertain (replayed), and "silent flips": decisions the product
+// lane would certify although they differ from the reference's -- which must never happen.  The ray always
 // follows the reference's decision, so its final RNG state and bounce count are the reference's
 // (tests compare them with the CPU oracle).
 #include <hip/hip_runtime.h>
@@ -61,8 +64,8 @@ __device__ __forceinline__ void atomic_max_pos(double *p, double v) {
 
 // Per-lane accumulators, flushed once per lane at the end.
 struct ShadowAcc {
-    uint64_t decisions = 0, uncertain = 0, flips = 0, bounces = 0;
-    double max_ratio = 0.0, max_ener = 0.0;
+    uint64_t decisions = 0, uncertain = 0, flips = 0, bounces = 0, fallbacks = 0;
+    double max_ratio = 0.0, max_ratio32 = 0.0, max_ener = 0.0;
     double max_depth[kDepthBuckets] = {0, 0, 0, 0, 0, 0};
     uint64_t n_depth[kDepthBuckets] = {0, 0, 0, 0, 0, 0};
     uint64_t hist[kHistBuckets] = {};
@@ -148,67 +151,56 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
             }
             hops = 0;
             const double4 cw = *(const double4 *)(JB + kJBlockCos);
-            const Rec k0 = load_rec(JB + kJBlockRec), k1 = load_rec(JB + kJBlockRec + 8);
-            const Rec k2 = three ? load_rec(JB + kJBlockRec + 16) : Rec{};
-            const JField f0 = jones(k0, jr), f1 = jones(k1, jr);
-            const double q0 = norm2(f0), q1 = norm2(f1), q2 = three ? norm2(jones(k2, jr)) : 0.0;
             const double jden = entry ? J[kJCosIc1] : cos_th;
             const double inv = rcp_nr(jden);
             const double f01 = entry ? A.n_g : 1.0;
-            const double a0 = q0 * cw.x * inv * f01, a1 = q1 * cw.y * inv * f01;
-            const double a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
-            const double c0 = a0, c1 = a0 + a1, c2 = c1 + a2;
             const double nb = (double)bounces * 0.01;
             const double en2 = fma(jr.er, jr.er, fma(jr.ei, jr.ei, fma(jr.mr, jr.mr, jr.mi * jr.mi)));
-            const double scl = A.cert_tol * fma(nb * nb, J[kJGrowth], 1.0) * fabs(inv) * fmax(en2, 1.0);
-            const double tol = scl * cw.w;
-            // how much of the bound the Jones arithmetic uses against the reference's thresholds
-            const double r0 = fabs(c0 - e0) / tol, r1 = fabs(c1 - (e0 + e1)) / tol;
-            const double r2 = three ? fabs(c2 - (e0 + e1 + e2)) / tol : 0.0;
-            const double ratio = tol > 1e-250 ? fmax(r0, fmax(r1, r2)) : 0.0;
-            bool ok = (tol > 1e-250) && fabs(u - c0) > tol && fabs(u - c1) > tol && (!three || fabs(u - c2) > tol);
-            bool p0 = true, p1 = true, p2 = true;
-            if (t == 0.0) {
-                ok = ok && (!thr || jener * tol > 1e-290);
-            } else if (thr) {
-                const double g0 = jener * a0, g1 = jener * a1, g2 = jener * a2;
-                const double re = eerr + 1e-15;
-                const double m0 = re * fabs(g0) + jener * scl * JB[kJBlockW] * 1.01;
-                const double m1 = re * fabs(g1) + jener * scl * JB[kJBlockW + 1] * 1.01;
-                const double m2 = re * fabs(g2) + jener * scl * JB[kJBlockW + 2] * 1.01;
-                p0 = g0 > t;
-                p1 = g1 > t;
-                p2 = g2 > t;
-                ok = ok && (u > c0 || fabs(g0 - t) > m0) && (u > c1 || fabs(g1 - t) > m1) &&
-                     (!three || u > c2 || fabs(g2 - t) > m2);
-                // the ener guard's tracked relative error against the reference's ener
-                const double er = fabs(jener / ener - 1.0) / re;
+            const double base = fma(nb * nb, J[kJGrowth], 1.0) * fabs(inv) * fmax(en2, 1.0);
+            const double c_ref[3] = {e0, e0 + e1, e0 + e1 + e2};
+            // how much of each bound the arithmetic uses against the reference's thresholds
+            auto ratio = [&](const JDecision &d, double scl) {
+                const double tol = scl * cw.w;
+                if (!(tol > 1e-250)) return 0.0;
+                const double c0 = d.a0, c1 = d.a0 + d.a1, c2 = c1 + d.a2;
+                const double r0 = fabs(c0 - c_ref[0]) / tol, r1 = fabs(c1 - c_ref[1]) / tol;
+                const double r2 = three ? fabs(c2 - c_ref[2]) / tol : 0.0;
+                return fmax(r0, fmax(r1, r2));
+            };
+            JDecision d32, d64;
+            estimate32(d32, JB, jr, three, inv, f01, A.inv_n_g, cw);
+            jones_decide(d32, u, A.cert_tol32 * base, JB, cw.w, three, thr, t, jener, eerr);
+            estimate64(d64, JB, jr, three, inv, f01, A.inv_n_g, cw);
+            jones_decide(d64, u, A.cert_tol * base, JB, cw.w, three, thr, t, jener, eerr);
+            const double r32 = ratio(d32, A.cert_tol32 * base), r64 = ratio(d64, A.cert_tol * base);
+            if (thr && t != 0.0) {   // the ener guard's tracked relative error against the reference's ener
+                const double er = fabs(jener / ener - 1.0) / (eerr + 1e-15);
                 acc.max_ener = fmax(acc.max_ener, er);
             }
-            const bool s0 = (u <= c0) && p0;
-            const bool s1 = !s0 && (u <= c1) && p1;
-            const bool s2 = !s0 && !s1 && three && (u <= c2) && p2;
-            const double n2 = s0 ? q0 : q1;
-            ok = ok && (!(s0 || s1) || n2 > 1e-300);
-            const int bj = s0 ? 0 : s1 ? 1 : s2 ? 2 : -1;
+            // the product lane's decision: the single-precision one, else the double-precision one
+            const JDecision &dd = d32.ok ? d32 : d64;
+            const int bj = dd.s0 ? 0 : dd.s1 ? 1 : dd.s2 ? 2 : -1;
             ++acc.decisions;
-            if (!ok) ++acc.uncertain;
+            if (!d32.ok) ++acc.fallbacks;
+            if (!dd.ok) ++acc.uncertain;
             else if (bj != b) ++acc.flips;
-            acc.max_ratio = fmax(acc.max_ratio, ratio);
+            acc.max_ratio = fmax(acc.max_ratio, r64);
+            acc.max_ratio32 = fmax(acc.max_ratio32, r32);
             const int db = depth_bucket(bounces);
-            acc.max_depth[db] = fmax(acc.max_depth[db], ratio);
+            acc.max_depth[db] = fmax(acc.max_depth[db], r32);
             ++acc.n_depth[db];
-            ++acc.hist[hist_bucket(ratio)];
-            // the product lane's state follows the reference's branch
+            ++acc.hist[hist_bucket(r32)];
+            // the product lane's state follows the reference's branch (its double-precision take)
             if (b == 0 || b == 1) {
-                const JField f = b == 0 ? f0 : f1;
-                const double rn = rsq_nr(b == 0 ? q0 : q1);
+                const JField f = jones(load_rec(JB + kJBlockRec + 8 * b), jr);
+                const double n2 = norm2(f);
+                const double rn = rsq_nr(n2);
                 jr.er = f.er * rn;
                 jr.ei = f.ei * rn;
                 jr.mr = f.mr * rn;
                 jr.mi = f.mi * rn;
-                const double ab = b == 0 ? a0 : a1;
-                if (t != 0.0) eerr += scl * JB[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+                const double ab = n2 * (b == 0 ? cw.x : cw.y) * inv * f01;
+                if (t != 0.0) eerr += A.cert_tol * base * JB[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
                 jener = jener * ab;
             }
         }
@@ -301,14 +293,16 @@ __global__ __launch_bounds__(256) void shadow_kernel(ShadowArgs S, Loc loc) {
     wgrt_shadow_stats *o = S.out;
     const bool lead = (threadIdx.x & 63) == 0;
     const uint64_t dec = wave_sum(acc.decisions), unc = wave_sum(acc.uncertain), fl = wave_sum(acc.flips);
-    const uint64_t bo = wave_sum(acc.bounces);
-    const double mr = wave_max(acc.max_ratio), me = wave_max(acc.max_ener);
+    const uint64_t bo = wave_sum(acc.bounces), fb = wave_sum(acc.fallbacks);
+    const double mr = wave_max(acc.max_ratio), mr32 = wave_max(acc.max_ratio32), me = wave_max(acc.max_ener);
     if (lead) {
         atomicAdd((unsigned long long *)&o->decisions, (unsigned long long)dec);
         atomicAdd((unsigned long long *)&o->uncertain, (unsigned long long)unc);
         atomicAdd((unsigned long long *)&o->silent_flips, (unsigned long long)fl);
         atomicAdd((unsigned long long *)&o->bounces, (unsigned long long)bo);
+        atomicAdd((unsigned long long *)&o->fallbacks, (unsigned long long)fb);
         atomic_max_pos(&o->max_ratio, mr);
+        atomic_max_pos(&o->max_ratio32, mr32);
         atomic_max_pos(&o->max_ener_ratio, me);
     }
     for (int k = 0; k < kDepthBuckets; ++k) {
@@ -365,7 +359,8 @@ extern "C" wgrt_status wgrt_debug_shadow(const wgrt_scene *s, const wgrt_rays *r
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
     A.threshold = single ? 1e-15 : 0.0;
-    A.cert_tol = wgrt_debug_set_cert_tol(0.0);   // the bound the product lane uses now (0: query only)
+    A.cert_tol = wgrt_debug_set_cert_tol(0.0);   // the bounds the product lane uses now (0: query only)
+    A.cert_tol32 = std::max(wgrt_debug_set_cert_tol32(0.0), A.cert_tol);
     S.out = stats;
     const int64_t blocks = std::min<int64_t>((n_rays + 255) / 256, 16384);
     hipLaunchKernelGGL(shadow_kernel<Locator>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, S, A.loc);

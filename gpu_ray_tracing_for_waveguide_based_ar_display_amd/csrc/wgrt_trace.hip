@@ -59,7 +59,11 @@ int g_jchunk = [] {
     const int c = v ? atoi(v) : 64;
     return c >= 64 ? c / 64 * 64 : 64;
 }();
-double g_cert_tol = 1e-10;   // Jones-vector variants' certification bound (wgrt_debug_set_cert_tol)
+double g_cert_tol = 1e-10;   // Jones-vector variants' double-precision certification bound (wgrt_debug_set_cert_tol)
+// ... and the single-precision estimate's (wgrt_debug_set_cert_tol32): 8e-6 covers the rounding of
+// |M E|^2 from float matrices and vector (about 26 ulp(1) of the bound's W scale) five times over;
+// wgrt_shadow.hip measures the margin
+double g_cert_tol32 = 8e-6;
 unsigned long long *g_timeline = nullptr;   // wgrt_debug_set_timeline
 // miss hops a lane may take per pass once the work queue is exhausted (env WGRT_DRAIN_HOPS)
 int g_drain_hops = [] {
@@ -794,6 +798,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
     A.cert_tol = g_cert_tol;
+    A.cert_tol32 = std::max(g_cert_tol32, g_cert_tol);   // raising the double bound raises this one too
     A.timeline = g_timeline;
     A.drain_hops = g_drain_hops;
     A.timeline_waves = g_timeline_waves;
@@ -1005,6 +1010,12 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
 void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves) {
     g_timeline = n_waves > 0 ? buf : nullptr;
     g_timeline_waves = n_waves > 0 ? n_waves : 0;
+}
+
+double wgrt_debug_set_cert_tol32(double cert_tol) {
+    const double prev = g_cert_tol32;
+    if (cert_tol > 0.0) g_cert_tol32 = cert_tol;
+    return prev;
 }
 
 double wgrt_debug_set_cert_tol(double cert_tol) {

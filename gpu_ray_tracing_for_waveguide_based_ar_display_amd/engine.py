@@ -237,10 +237,11 @@ def shadow(scene: Scene, rays: dict, rng_states: torch.Tensor, gid_offset: int =
     host = buf.cpu().numpy()
     st = _lib.ShadowStats.from_buffer_copy(host.tobytes())
     return {"decisions": st.decisions, "uncertain": st.uncertain, "silent_flips": st.silent_flips,
-            "bounces": st.bounces, "max_ratio": st.max_ratio,
-            "max_ratio_by_depth": dict(zip(SHADOW_DEPTHS, list(st.max_ratio_by_depth))),
+            "bounces": st.bounces, "fallbacks": st.fallbacks, "max_ratio": st.max_ratio,
+            "max_ratio32": st.max_ratio32,
+            "max_ratio32_by_depth": dict(zip(SHADOW_DEPTHS, list(st.max_ratio_by_depth))),
             "decisions_by_depth": dict(zip(SHADOW_DEPTHS, [int(v) for v in st.decisions_by_depth])),
-            "ratio_hist_log10": {f"1e{b - 18}": int(v) for b, v in enumerate(st.ratio_hist) if v},
+            "ratio32_hist_log10": {f"1e{b - 18}": int(v) for b, v in enumerate(st.ratio_hist) if v},
             "max_ener_ratio": st.max_ener_ratio}
 
 

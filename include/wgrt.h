@@ -230,6 +230,10 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
  * larger values make more decisions uncertain and send more rays through the replay kernel,
  * results unchanged).  Process-wide; returns the previous value (a value <= 0 only queries). */
 double wgrt_debug_set_cert_tol(double cert_tol);
+/* Test hook: base of the single-precision estimate's bound (default 8e-6; the effective value is
+ * max(this, cert_tol)).  Larger values send more decisions through the double-precision
+ * re-evaluation (results unchanged).  Process-wide; returns the previous value (<= 0 queries). */
+double wgrt_debug_set_cert_tol32(double cert_tol);
 
 /* Certification shadow of the Jones-vector variants (diagnostic; wgrt_shadow.hip).  Traces rays
  * [0, n_rays) with the reference's own arithmetic (unwrapped delta_phase, hypot / atan2 / wrap,
@@ -243,11 +247,13 @@ typedef struct {
     uint64_t uncertain;          /* decisions the Jones lane cannot certify (its rays are replayed)   */
     uint64_t silent_flips;       /* certified Jones decisions that differ from the reference's: 0    */
     uint64_t bounces;            /* ray-bounce events traced                                          */
-    double max_ratio;            /* max over decisions / thresholds of |c_jones - c_ref| / tol        */
-    double max_ratio_by_depth[6];   /* the same by bounce depth [1,10) [10,30) [30,100) [100,300)
+    uint64_t fallbacks;          /* decisions the single-precision estimate leaves to the double one  */
+    double max_ratio;            /* max over decisions / thresholds of |c_jones64 - c_ref| / tol64    */
+    double max_ratio32;          /* the same for the single-precision estimate against tol32          */
+    double max_ratio_by_depth[6];   /* max_ratio32 by bounce depth [1,10) [10,30) [30,100) [100,300)
                                        [300,1000) [1000,inf)                                          */
     uint64_t decisions_by_depth[6];
-    uint64_t ratio_hist[20];     /* decisions by log10 of their max ratio: bucket b = [1e(b-18),
+    uint64_t ratio_hist[20];     /* decisions by log10 of their ratio32: bucket b = [1e(b-18),
                                     1e(b-17)); bucket 0 also holds smaller ratios, 19 larger ones    */
     double max_ener_ratio;       /* single wavelength: max |ener_jones / ener_ref - 1| / tracked bound */
 } wgrt_shadow_stats;
