@@ -128,13 +128,17 @@ def load(path: str = LIB_PATH):
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
     L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
-    L.wgrt_debug_shadow.restype = st
-    L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp, _vp,
-                                    _vp, _vp]
-    L.wgrt_debug_set_timeline.restype = None
-    L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
-    L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
-    L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]
+    # debug / test hooks: optional, so tools can load older builds of the library (tools/ab.py)
+    if hasattr(L, "wgrt_debug_shadow"):
+        L.wgrt_debug_shadow.restype = st
+        L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
+                                        _vp, _vp, _vp]
+    if hasattr(L, "wgrt_debug_set_timeline"):
+        L.wgrt_debug_set_timeline.restype = None
+        L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
+    if hasattr(L, "wgrt_debug_set_cert_tol32"):
+        L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
+        L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]
     L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
     L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
     L.wgrt_status_string.restype = ctypes.c_char_p

@@ -66,7 +66,6 @@ struct TraceArgs {
     unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
     unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_set_timeline), NULL normally
     int64_t timeline_waves;
-    int drain_hops;                     // miss hops per pass once the work queue is exhausted
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;
@@ -827,12 +826,26 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
     const double t = A.threshold;
     JDecision d;
+#ifdef WGRT_EXP_EST64
+    // experiment: all-double estimate with the matrices loaded up front (round-1 arithmetic)
+    const Rec k0 = load_rec(B + kJBlockRec), k1 = load_rec(B + kJBlockRec + 8);
+    Rec k2{};
+    if (three) k2 = load_rec(B + kJBlockRec + 16);
+    const JField f0 = jones(k0, r), f1 = jones(k1, r);
+    const double q0 = norm2(f0), q1 = norm2(f1);
+    const double q2 = three ? norm2(jones(k2, r)) : 0.0;
+    d.a0 = q0 * cw.x * inv * f01;
+    d.a1 = q1 * cw.y * inv * f01;
+    d.a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
+    jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, r.eerr);
+#else
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, r.eerr);
     if (!d.ok) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
         jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, r.eerr);
     }
+#endif
     // one exit for every outcome but a taken branch; an out-coupling is appended to the
     // out-coupling queue by the caller (at (r.x, r.y))
     const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
@@ -840,7 +853,11 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const bool ba = d.s0;
     const int b = ba ? 0 : 1;
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
+#ifdef WGRT_EXP_EST64
+    const JField f = ba ? f0 : f1;
+#else
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
+#endif
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
     const double rn = rsq_nr(n2);
@@ -858,10 +875,20 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.y = ba ? ya : yb;
     r.gx = ba ? mva.x : mvb.x;
     r.gy = ba ? mva.y : mvb.y;
+#ifdef WGRT_EXP_NODEFER
+    L.pfa = ba ? pa : pb;
+    L.pfsel = true;
+    if (kind == 0) {
+        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pfa, kPolyIC, r.x, r.y);
+        if (ba) return in_ic ? 0 : 2;
+        return in_ic ? 1 : kDie;
+    }
+#else
     L.pfa = pa;
     L.pfb = pb;
     L.pfsel = ba;
     if (kind == 0) return ba ? kRegionIcA : kRegionIcB;   // in-coupler test at the next pass
+#endif
     if (kind <= 2) return ba ? 2 : 3;
     return ba ? 4 : 5;
 }

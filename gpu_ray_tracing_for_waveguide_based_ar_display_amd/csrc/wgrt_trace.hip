@@ -65,11 +65,7 @@ double g_cert_tol = 1e-10;   // Jones-vector variants' double-precision certific
 // wgrt_shadow.hip measures the margin
 double g_cert_tol32 = 8e-6;
 unsigned long long *g_timeline = nullptr;   // wgrt_debug_set_timeline
-// miss hops a lane may take per pass once the work queue is exhausted (env WGRT_DRAIN_HOPS)
-int g_drain_hops = [] {
-    const char *v = getenv("WGRT_DRAIN_HOPS");
-    return v ? atoi(v) : 1;
-}();
+
 int64_t g_timeline_waves = 0;
 
 
@@ -234,12 +230,13 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     unsigned long long pend_v = 0;    // its result (lane 0)
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
     // debug timeline (wgrt_debug_set_timeline; NULL in production): per wave, start / queue
-    // exhausted / end (s_memrealtime, 100 MHz), passes, and lane-passes with a ray in flight
+    // exhausted / end (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD,
+    // and the passes / lane-passes up to the queue running dry
     unsigned long long *const tl = KA(timeline);
     const int64_t tl_wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
     const bool tl_on = tl != nullptr && tl_wave < KA(timeline_waves);
     unsigned long long tl_passes = 0, tl_lanes = 0;
-    if (tl_on && lane == 0) tl[6 * tl_wave] = __builtin_amdgcn_s_memrealtime();
+    if (tl_on && lane == 0) tl[8 * tl_wave] = __builtin_amdgcn_s_memrealtime();
     uint32_t cur_k = 0;               // the item's iteration
     bool exhausted = false;
     bool active = false, waiting = false;
@@ -303,10 +300,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
     for (;;) {
         if (active) {
-            // once the queue has run dry a lane may take several miss hops per pass (g_drain_hops): the
-            // wave's interaction step no longer competes with refills, and a drain-phase ray's
-            // chain of passes is the launch's critical path
-            blk = (exhausted && A.drain_hops > 1) ? advance(A, loc, L, kind, A.drain_hops) : advance(A, loc, L, kind);
+            blk = advance(A, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
@@ -356,7 +350,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 pend_h = -1;
                 if (!got) {
                     exhausted = true;
-                    if (tl_on && lane == 0) tl[6 * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
+                    if (tl_on && lane == 0) {
+                        tl[8 * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
+                        tl[8 * tl_wave + 6] = tl_passes;
+                        tl[8 * tl_wave + 7] = tl_lanes;
+                    }
                     break;
                 }
                 pend_h = head;   // issue the next dequeue now; read when this item runs dry
@@ -433,10 +431,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     }
     for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
     if (tl_on && lane == 0) {
-        tl[6 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
-        tl[6 * tl_wave + 3] = tl_passes;
-        tl[6 * tl_wave + 4] = tl_lanes;
-        tl[6 * tl_wave + 5] = (unsigned long long)xcc_id();
+        tl[8 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
+        tl[8 * tl_wave + 3] = tl_passes;
+        tl[8 * tl_wave + 4] = tl_lanes;
+        tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
     }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
     __shared__ unsigned long long red[4][2];
@@ -800,7 +798,6 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.cert_tol = g_cert_tol;
     A.cert_tol32 = std::max(g_cert_tol32, g_cert_tol);   // raising the double bound raises this one too
     A.timeline = g_timeline;
-    A.drain_hops = g_drain_hops;
     A.timeline_waves = g_timeline_waves;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;

@@ -263,8 +263,9 @@ wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, in
                               void *stream);
 
 /* Debug hook (process-wide): while set, every Jones-vector launch records, per wave w < n_waves
- * of its grid, 6 words into the DEVICE buffer buf[6 w ..]: start, queue-exhausted and end times
- * (s_memrealtime, 100 MHz), passes of the wave loop, lane-passes with a ray in flight, XCD id.
+ * of its grid, 8 words into the DEVICE buffer buf[8 w ..]: start, queue-exhausted and end times
+ * (s_memrealtime, 100 MHz), passes of the wave loop, lane-passes with a ray in flight, XCD id,
+ * and the passes and lane-passes before the queue ran dry.
  * buf = NULL or n_waves = 0 turns it off (the default). */
 void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves);
 

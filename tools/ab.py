@@ -1,0 +1,84 @@
+#!/usr/bin/env python3
+"""A/B timing of library builds (exp_libs/<name>/libwgrt.so, tools/ab_build.py) on the bench
+workload: rounds of one subprocess per build (WGRT_LIB), interleaved, each timing `--launches`
+single-trace launches and one fused `--fused`-trace call with HIP events; prints the per-build
+medians.  Usage: python tools/ab.py NAME [NAME ...] [--rounds 4] [--config C3]"""
+import argparse
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+CHILD = r'''
+import json, os, sys
+import numpy as np
+sys.path.insert(0, os.environ["REPO"])
+import torch, bench
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, trace_fullcolor, reserve
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+cfg = bench.CONFIGS[os.environ["AB_CONFIG"]]
+nx, ny, lam, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
+dev = torch.device("cuda", 0)
+g = design_geometry(nx, ny); L = synthetic_luts(g, seed=0, profile=cfg["profile"])
+pts = generate_points_in_polygon(g.IC, R // 2, rng=np.random.default_rng(1))
+sc = Scene.from_geometry(g, L)
+rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(0, nx * ny * len(lam))
+eb = torch.zeros(sc.eb_shape(), dtype=torch.float32, device=dev)
+st = torch.zeros(4, dtype=torch.int64, device=dev)
+nl, nf = int(os.environ["AB_LAUNCHES"]), int(os.environ["AB_FUSED"])
+reserve(sc, rays["x"].numel(), nf)
+for _ in range(3): trace_fullcolor(sc, rays, rng, eb)
+trace_fullcolor(sc, rays, rng, eb, num_iter=2)
+torch.cuda.synchronize()
+ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl + 1)]
+st.zero_()
+for k in range(nl):
+    ev[k][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st); ev[k][1].record()
+torch.cuda.synchronize()
+b1 = int(st[0]) / nl
+st.zero_()
+ev[nl][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st, num_iter=nf); ev[nl][1].record()
+torch.cuda.synchronize()
+single = [ev[k][0].elapsed_time(ev[k][1]) for k in range(nl)]
+print(json.dumps({"single_ms": float(np.median(single)), "fused_ms_per_step": ev[nl][0].elapsed_time(ev[nl][1]) / nf,
+                  "bounces_per_launch": b1, "fused_bounces": int(st[0])}))
+'''
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("names", nargs="+")
+    ap.add_argument("--rounds", type=int, default=4)
+    ap.add_argument("--config", default="C3")
+    ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--fused", type=int, default=20)
+    a = ap.parse_args()
+    res = {n: [] for n in a.names}
+    for r in range(a.rounds):
+        for n in a.names:
+            lib = os.path.join(REPO, "exp_libs", n, "libwgrt.so") if n != "tree" else ""
+            env = dict(os.environ, REPO=REPO, AB_CONFIG=a.config, AB_LAUNCHES=str(a.launches),
+                       AB_FUSED=str(a.fused), WGRT_LIB=lib)
+            p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+            if p.returncode:
+                print(p.stderr[-3000:])
+                sys.exit(p.returncode)
+            d = json.loads(p.stdout.strip().splitlines()[-1])
+            res[n].append(d)
+            print(r, n, json.dumps(d), flush=True)
+    for n, v in res.items():
+        s = np.median([d["single_ms"] for d in v])
+        f = np.median([d["fused_ms_per_step"] for d in v])
+        b = v[0]["bounces_per_launch"]
+        print(f"SUMMARY {n}: single {s:.4f} ms ({b / s / 1e6:.3e} b/s), fused {f:.4f} ms/step ({b / f / 1e6:.3e} b/s)")
+
+
+if __name__ == "__main__":
+    main()

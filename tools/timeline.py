@@ -47,7 +47,7 @@ def main():
     rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(0, nx * ny * len(lam))
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     nw = 256 * 8 * 4 * 2
-    buf = torch.zeros(6 * nw, dtype=torch.int64, device=dev)
+    buf = torch.zeros(8 * nw, dtype=torch.int64, device=dev)
     L = _lib.load()
     order = None
     if a.order == "lifetime":
@@ -68,9 +68,9 @@ def main():
         e1.record()
         torch.cuda.synchronize()
         L.wgrt_debug_set_timeline(None, 0)
-        t = buf.cpu().numpy().reshape(-1, 6)
+        t = buf.cpu().numpy().reshape(-1, 8)
         t = t[t[:, 0] > 0]
-        start, exh, end, passes, lanes, xcc = (t[:, k].astype(np.float64) for k in range(6))
+        start, exh, end, passes, lanes, xcc, p_exh, l_exh = (t[:, k].astype(np.float64) for k in range(8))
         t0 = start.min()
         us = lambda v: (v - t0) / 100.0   # 100 MHz ticks -> us
         r = {"event_ms": e0.elapsed_time(e1), "waves": int(len(t)),
@@ -79,6 +79,13 @@ def main():
              "end_us": [float(np.percentile(us(end), q)) for q in (0, 10, 50, 90, 99, 100)],
              "passes_per_wave": [float(np.percentile(passes, q)) for q in (0, 50, 100)],
              "mean_active_lanes_per_pass": float(lanes.sum() / max(passes.sum(), 1)),
+             "bulk_us_per_pass": float(np.median(us(exh) / np.maximum(p_exh, 1))),
+             "drain_us_per_pass": float(np.median((end - exh) / 100.0 / np.maximum(passes - p_exh, 1))),
+             "drain_passes": [float(np.percentile(passes - p_exh, q)) for q in (0, 50, 100)],
+             "drain_lanes_per_pass": float((lanes - l_exh).sum() / max((passes - p_exh).sum(), 1)),
+             "bulk_lanes_per_pass": float(l_exh.sum() / max(p_exh.sum(), 1)),
+             "waves_alive_at_us": {int(tt): int(((us(start) <= tt) & (us(end) > tt)).sum())
+                                   for tt in (100, 200, 250, 300, 350, 400)},
              "end_by_xcd_us": {int(x): float(us(end[xcc == x]).max()) for x in np.unique(xcc)},
              "exhausted_by_xcd_us": {int(x): float(us(exh[xcc == x]).max()) for x in np.unique(xcc)}}
         r["order"] = a.order
