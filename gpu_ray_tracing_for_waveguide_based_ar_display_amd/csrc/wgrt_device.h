@@ -575,22 +575,13 @@ struct JRay {
 
 struct JLane {
     JRay r;
-    const double *T;         // this ray's Jones tile
-    int64_t i;
+    uint32_t tix;            // this ray's (lambda, m, n) tile index (its Jones tile: jtiles + tix * jtile_d)
+    uint32_t i;              // local ray index (variants 7 / 9: < 2^32)
     uint32_t bounces;
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
-    // locator cell word of (x, y), loaded a step ahead: an interaction loads the words of both
-    // candidate positions and keeps both, the choice is resolved where the word is used (next
-    // pass), so the interaction never waits for those loads
-    uint64_t pfa, pfb;
-    bool pfsel;              // true: pfa
+    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
-
-// Regions 6 / 7: an in-coupler state's branch was taken and the in-coupler test at the new
-// position (GRTF:883-900, 928-949, 974-995) is still to be made -- at the next pass, on the
-// prefetched cell word: 6 -> R0 if inside the IC else R2; 7 -> R1 if inside, else the ray dies.
-constexpr int kRegionIcA = 6, kRegionIcB = 7;
 
 enum : int { kUncertain = -3, kOut = -4 };
 
@@ -611,8 +602,8 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int m = (int)fm, n = (int)fn, l = (int)fl;
     const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
-    L.i = i;
-    L.T = KA(jtiles) + (ok ? (int64_t)((l * A.nx + m) * A.ny + n) * A.jtile_d : 0);
+    L.i = (uint32_t)i;
+    L.tix = ok ? (uint32_t)((l * A.nx + m) * A.ny + n) : 0u;
     L.r.x = (double)fx;
     L.r.y = (double)fy;
     const double te = (double)fte, tm = (double)ftm;
@@ -631,8 +622,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.r.s = rs;
     L.r.region = 0;
     L.bounces = 1;
-    L.pfa = L.pfb = 0ull;
-    L.pfsel = true;
+    L.pf = 0ull;
     return ok;
 }
 
@@ -790,74 +780,61 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // abandoned.  The taken branch's field is always computed in double precision from its
 // double-precision matrix (loaded after the decision), so the carried Jones vector and ener
 // are the same values the all-double evaluation gives.
-template <class Loc>
+template <bool SINGLE, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
                                         bool entry) {
     JRay &r = L.r;
-    const double *T = L.T;
+    const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
     const bool three = kind >= 3;
     const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
+    const double t = SINGLE ? A.threshold : 0.0;
     // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
     // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    const double2 mva = *(const double2 *)(T + kJGap + ga), mvb = *(const double2 *)(T + kJGap + gb);
-    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
-    const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
-    const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
-    const double xa = r.x + mva.x, ya = r.y + mva.y;
-    const double xb = r.x + mvb.x, yb = r.y + mvb.y;
-    const uint64_t pa = locate_c(loc, xa, ya), pb = locate_c(loc, xb, yb);
-
-    // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
-    for (uint32_t h = 0; h < r.hops; ++h) {
-        const double mr = r.mr;
-        r.mr = fma(mr, hop.x, -r.mi * hop.y);
-        r.mi = fma(mr, hop.y, r.mi * hop.x);
+    uint64_t pa, pb;
+    {   // the cell words of both candidate next positions, issued first (read at the take)
+        const double2 mva = *(const double2 *)(T + kJGap + ga), mvb = *(const double2 *)(T + kJGap + gb);
+        pa = locate_c(loc, r.x + mva.x, r.y + mva.y);
+        pb = locate_c(loc, r.x + mvb.x, r.y + mvb.y);
     }
-    r.hops = 0;
+    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
+    const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
+    // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
+    if (r.hops) {
+        const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
+        for (uint32_t h = 0; h < r.hops; ++h) {
+            const double mr = r.mr;
+            r.mr = fma(mr, hop.x, -r.mi * hop.y);
+            r.mi = fma(mr, hop.y, r.mi * hop.x);
+        }
+        r.hops = 0;
+    }
     const double denom = entry ? cg.x : r.cos_t;
-    const double u = rng_draw(r.s, A.gid_offset + L.i);
+    const double u = rng_draw(r.s, A.gid_offset + (int64_t)L.i);
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
     const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
-    const double t = A.threshold;
     JDecision d;
-#ifdef WGRT_EXP_EST64
-    // experiment: all-double estimate with the matrices loaded up front (round-1 arithmetic)
-    const Rec k0 = load_rec(B + kJBlockRec), k1 = load_rec(B + kJBlockRec + 8);
-    Rec k2{};
-    if (three) k2 = load_rec(B + kJBlockRec + 16);
-    const JField f0 = jones(k0, r), f1 = jones(k1, r);
-    const double q0 = norm2(f0), q1 = norm2(f1);
-    const double q2 = three ? norm2(jones(k2, r)) : 0.0;
-    d.a0 = q0 * cw.x * inv * f01;
-    d.a1 = q1 * cw.y * inv * f01;
-    d.a2 = three ? q2 * cw.z * inv * A.inv_n_g : 0.0;
-    jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, r.eerr);
-#else
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
-    jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, r.eerr);
+    jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     if (!d.ok) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
-        jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, r.eerr);
+        jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     }
-#endif
     // one exit for every outcome but a taken branch; an out-coupling is appended to the
     // out-coupling queue by the caller (at (r.x, r.y))
     const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
     if (code != 0) return code;
     const bool ba = d.s0;
     const int b = ba ? 0 : 1;
-    // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
-#ifdef WGRT_EXP_EST64
-    const JField f = ba ? f0 : f1;
-#else
+    // the taken branch: its double-precision matrix and its move, loaded now (L1 / L2-hot)
+    const double2 mv = *(const double2 *)(T + kJGap + (ba ? ga : gb));
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
-#endif
+    // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
     const double rn = rsq_nr(n2);
@@ -868,47 +845,33 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double ab = n2 * (ba ? cw.x : cw.y) * inv * f01;   // the taken branch's efficiency, double precision
     // ener accumulates every taken branch's relative error, the in-coupler states' too (no guard there,
     // but their factors are part of ener at every later guard)
-    if (t != 0.0) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
+    if (SINGLE) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
-    r.x = ba ? xa : xb;
-    r.y = ba ? ya : yb;
-    r.gx = ba ? mva.x : mvb.x;
-    r.gy = ba ? mva.y : mvb.y;
-#ifdef WGRT_EXP_NODEFER
-    L.pfa = ba ? pa : pb;
-    L.pfsel = true;
+    r.x = r.x + mv.x;   // the same operation that formed the candidate's cell address
+    r.y = r.y + mv.y;
+    r.gx = mv.x;
+    r.gy = mv.y;
+    L.pf = ba ? pa : pb;
     if (kind == 0) {
-        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pfa, kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
-#else
-    L.pfa = pa;
-    L.pfb = pb;
-    L.pfsel = ba;
-    if (kind == 0) return ba ? kRegionIcA : kRegionIcB;   // in-coupler test at the next pass
-#endif
     if (kind <= 2) return ba ? 2 : 3;
     return ba ? 4 : 5;
 }
 
 // Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
 // that need no Monte-Carlo interaction, at most kJMaxHops per call: every iteration then tests
-// a cell word loaded a pass earlier (JLane::pfa / pfb), and a hop issues the load of the next one.  1 measured
+// a cell word loaded a pass earlier (JLane::pf), and a hop issues the load of the next one.  1 measured
 // best on C3 (2 and 4 slower); a compile-time bound, not a kernarg, straightens the loop (-2 %
 // fused).
 constexpr int kJMaxHops = 1;
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind, int max_hops = kJMaxHops) {
     JRay &r = L.r;
-    auto c = (typename Loc::Word)(L.pfsel ? L.pfa : L.pfb);
-    if (r.region >= kRegionIcA) {   // the pending in-coupler test of the last interaction
-        const bool in_ic = in_poly_w<true>(loc, c, kPolyIC, r.x, r.y);
-        if (r.region == kRegionIcA) r.region = in_ic ? 0 : 2;
-        else if (in_ic) r.region = 1;
-        else return kDie;   // GRTF:899-900, 948-949, 994-995
-    }
+    auto c = (typename Loc::Word)L.pf;
     for (int hops = 0;; ++hops) {
         if (hops >= max_hops) return kTransit;
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
@@ -937,8 +900,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         r.y = r.y + r.gy;
         ++r.hops;
         c = locate_c(loc, r.x, r.y);   // used from the next pass on (or the next hop of this call)
-        L.pfa = c;
-        L.pfsel = true;
+        L.pf = c;
     }
 }
 

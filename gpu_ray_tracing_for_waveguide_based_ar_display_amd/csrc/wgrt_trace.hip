@@ -219,10 +219,9 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
 // (waiting in place, lane idle, until the tag says k) -- the granule hand-off of
 // MI355X_MICROARCH.md's price list, valid whatever the XCD placement.  Results are identical
 // to n_iter launches: each ray's traces run in order from the same states; eyebox adds commute.
-template <bool FUSED, class Loc>
+template <bool FUSED, bool SINGLE, class Loc>
 __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, unsigned long long *heads, int chunk) {
     const int lane = threadIdx.x & 63;
-    const uint64_t lt_mask = (lane == 0) ? 0ull : (~0ull >> (64 - lane));
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
     int head = xcc_id();
@@ -243,7 +242,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
-    uint64_t tot_b = 0, tot_bad = 0;   // per lane, over every trace the lane runs
+    // per-lane totals in 32 bits: a lane's bounce total is added to the stats directly before it
+    // could overflow (2^31 bounces on one lane: never in practice)
+    uint32_t tot_b = 0, tot_bad = 0;
     uint32_t wait_passes = 0;          // fused: passes spent waiting for the current ray
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
@@ -287,6 +288,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     };
     auto retire = [&]() {
         tot_b += L.bounces;
+        if (tot_b >= 0x80000000u) {
+            wgrt_trace_stats *const st = KA(stats);
+            if (st) atomicAdd((unsigned long long *)&st->bounces, (unsigned long long)tot_b);
+            tot_b = 0;
+        }
         if (FUSED && (int64_t)L.k + 1 < n_iter) {
             __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
                                __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -370,7 +376,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             const int64_t avail = end - cur;
             const int take = (int64_t)want < avail ? want : (int)avail;
             if (!active && !waiting) {
-                const int rank = __popcll(need & lt_mask);
+                const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
                 if (rank < take) {
                     L.i = cur + rank;
                     L.k = cur_k;
@@ -387,7 +393,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         bool out = false;
         if (active && blk >= 0) {
-            const int next = interact(A, loc, L, blk, kind, entry);
+            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
                 retire();
@@ -410,7 +416,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // once per hundred passes)
         const uint64_t om = __ballot(out);
         if (om != 0ull) {
-            const int nout = __popcll(om), rank = __popcll(om & lt_mask), rem = kQBlock - qfill;
+            const int nout = __popcll(om), rem = kQBlock - qfill;
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0));
             unsigned long long nb = 0;
             if (nout > rem) {
                 if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
@@ -419,7 +426,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
                 const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
                 KA(q_xy)[j] = double2{L.r.x, L.r.y};
-                KA(q_i)[j] = (uint32_t)((L.T - KA(jtiles)) / A.jtile_d);
+                KA(q_i)[j] = L.tix;
             }
             if (nout > rem) {
                 qbase = nb;
@@ -438,11 +445,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
     __shared__ unsigned long long red[4][2];
-    tot_b = wave_sum(tot_b);
-    tot_bad = wave_sum(tot_bad);
+    const uint64_t sum_b = wave_sum((uint64_t)tot_b);
+    const uint64_t sum_bad = wave_sum((uint64_t)tot_bad);
     if (lane == 0) {
-        red[threadIdx.x >> 6][0] = tot_b;
-        red[threadIdx.x >> 6][1] = tot_bad;
+        red[threadIdx.x >> 6][0] = sum_b;
+        red[threadIdx.x >> 6][1] = sum_bad;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -456,11 +463,16 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
 // Variants 7 / 9: the persistent loop over the Jones-vector path, 3 waves per SIMD (32-bit cell
 // words; 64-bit cell words for scenes of more than 16 polygons).
-constexpr int kJonesWaves = 3;
-template <class CellT, bool FUSED>
-__global__ __launch_bounds__(256, kJonesWaves) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
+#ifndef WGRT_JONES_WAVES
+#define WGRT_JONES_WAVES 4         // waves per SIMD of the single-trace kernels (<= 128 VGPRs)
+#endif
+#ifndef WGRT_JONES_FUSED_WAVES
+#define WGRT_JONES_FUSED_WAVES 3   // ... of the fused ones (their hand-off state does not fit 128)
+#endif
+template <class CellT, bool FUSED, bool SINGLE>
+__global__ __launch_bounds__(256, FUSED ? WGRT_JONES_FUSED_WAVES : WGRT_JONES_WAVES) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    jones_body<FUSED>(A, loc, counter, chunk);
+    jones_body<FUSED, SINGLE>(A, loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -597,10 +609,17 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     {
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint32_t, false>, 256, 0));
-        s->jones_grid = std::max(1, cus * std::max(1, per_cu));
-        HIP_TRY(hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, trace_jones_kernel<uint64_t, false>, 256, 0));
-        s->jones64_grid = std::max(1, cus * std::max(1, per_cu));
+        // resident workgroups of each instantiation (cell width x fused; the single-wavelength
+        // kernels have their full-colour twins' register budgets)
+        auto grid_of = [&](const void *k, int &out) -> hipError_t {
+            const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0);
+            out = std::max(1, cus * std::max(1, per_cu));
+            return e;
+        };
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint32_t, false, false>, s->jones_grid[0][0]));
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint32_t, true, false>, s->jones_grid[0][1]));
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint64_t, false, false>, s->jones_grid[1][0]));
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint64_t, true, false>, s->jones_grid[1][1]));
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
@@ -810,7 +829,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         HIP_TRY(hipGetLastError());
         return WGRT_OK;
     }
-    int64_t grid = workgroups > 0 ? workgroups : (variant == 7 ? s->jones_grid : s->jones64_grid);
+    int64_t grid = workgroups > 0 ? workgroups : s->jones_grid[variant == 9][num_iter > 1];
     const int64_t useful = (n_rays + 255) / 256;
     if (grid > useful) grid = useful;
     wgrt_scene *ms = const_cast<wgrt_scene *>(s);
@@ -835,18 +854,25 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
     const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
     const dim3 g3((unsigned)grid), b3(256);
+    // instantiations: cell word width x fused chain x single-wavelength guard
+#define WGRT_LAUNCH_JONES(CELL, LOCV)                                                                              \
+    do {                                                                                                           \
+        if (num_iter > 1 && single)                                                                                \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, true>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk);  \
+        else if (num_iter > 1)                                                                                     \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, false>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk); \
+        else if (single)                                                                                           \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, true>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk); \
+        else                                                                                                       \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk);\
+    } while (0)
     if (variant == 9) {
-        if (num_iter > 1)
-            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, true>), g3, b3, 0, st, A, A.loc, sc->ctr, jchunk);
-        else
-            hipLaunchKernelGGL((trace_jones_kernel<uint64_t, false>), g3, b3, 0, st, A, A.loc, sc->ctr, jchunk);
+        WGRT_LAUNCH_JONES(uint64_t, A.loc);
     } else {
         const LocatorT<uint32_t> l32 = make_locator32(s);
-        if (num_iter > 1)
-            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, true>), g3, b3, 0, st, A, l32, sc->ctr, jchunk);
-        else
-            hipLaunchKernelGGL((trace_jones_kernel<uint32_t, false>), g3, b3, 0, st, A, l32, sc->ctr, jchunk);
+        WGRT_LAUNCH_JONES(uint32_t, l32);
     }
+#undef WGRT_LAUNCH_JONES
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
     HIP_TRY(hipGetLastError());
@@ -863,7 +889,8 @@ wgrt_status wgrt_scene_reserve(const wgrt_scene *s, int64_t n_rays, int num_iter
     if (!s) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene");
     if (n_rays < 0 || num_iter < 0 || num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "bad n_rays / num_iter");
     if (n_rays == 0) return WGRT_OK;
-    const int64_t grid = std::max<int64_t>(s->jones_grid, s->jones64_grid);
+    const int64_t grid = std::max(std::max(s->jones_grid[0][0], s->jones_grid[0][1]),
+                                  std::max(s->jones_grid[1][0], s->jones_grid[1][1]));
     wgrt_scene::Scratch *sc = nullptr;
     return ensure_scratch(const_cast<wgrt_scene *>(s), stream, n_rays, std::max(num_iter, 1),
                           std::min<int64_t>(grid, (n_rays + 255) / 256), &sc);
