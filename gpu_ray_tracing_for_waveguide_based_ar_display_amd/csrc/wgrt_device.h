@@ -553,13 +553,13 @@ __device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int
 // reference-arithmetic path (the epilogue kernel).  Positions, hop counts and eyebox indices are the
 // reference's exact float64 operations, as in every other variant.
 //
-// Latency and issue: a ray's bounces form one dependent chain (cell word -> block -> math ->
-// next position) and a launch's tail is the chain of its longest-lived rays, so every pass is
-// built to wait for one batch of loads: an interaction loads its whole block (the TIR step of
-// each taken branch is pre-folded into the block's TM rows, wgrt_common.h kJ*), the two
-// candidate moves, and issues the cell-word loads of both candidate next positions; a miss hop
-// only moves (its phase steps are applied as a power at the next interaction) and issues the
-// cell load of its new position, read in the next pass (JLane::pf).  Out-coupled
+// Latency and traffic: a ray's bounces form one dependent chain (cell word -> block -> math ->
+// next position).  An interaction loads its block's single-precision part (the TIR step of each
+// taken branch is pre-folded into the block's TM rows, wgrt_common.h kJ*), decides, then loads
+// the taken branch's double-precision matrix and issues the cell-word load of the new position;
+// a miss hop only moves (its phase steps are applied as a power at the next interaction) and
+// issues the cell load of its new position.  Either cell word is read in the next pass
+// (JLane::pf), so its latency overlaps the rest of the pass and the other waves'.  Out-coupled
 // rays are queued (position + ray index) and binned into matrix_EB by the epilogue kernel, so
 // the eyebox predicate and its divisions stay out of the wave loop.
 struct JRay {
@@ -793,12 +793,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    uint64_t pa, pb;
-    {   // the cell words of both candidate next positions, issued first (read at the take)
-        const double2 mva = *(const double2 *)(T + kJGap + ga), mvb = *(const double2 *)(T + kJGap + gb);
-        pa = locate_c(loc, r.x + mva.x, r.y + mva.y);
-        pb = locate_c(loc, r.x + mvb.x, r.y + mvb.y);
-    }
     const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
@@ -848,11 +842,15 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     if (SINGLE) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
-    r.x = r.x + mv.x;   // the same operation that formed the candidate's cell address
+    r.x = r.x + mv.x;
     r.y = r.y + mv.y;
     r.gx = mv.x;
     r.gy = mv.y;
-    L.pf = ba ? pa : pb;
+    // the new position's cell word, read by the next pass's advance().  Only the taken
+    // branch's: issuing both candidates' before the decision hid this load's latency but doubled
+    // the cell-word gathers, and those (random 4-B reads of a 71 MB grid, L2 misses) are what the
+    // passes queue behind -- loading one after the decision measured 11 % faster on C3
+    L.pf = locate_c(loc, r.x, r.y);
     if (kind == 0) {
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;

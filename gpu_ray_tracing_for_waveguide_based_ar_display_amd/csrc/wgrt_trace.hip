@@ -461,16 +461,19 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     }
 }
 
-// Variants 7 / 9: the persistent loop over the Jones-vector path, 3 waves per SIMD (32-bit cell
-// words; 64-bit cell words for scenes of more than 16 polygons).
+// Variants 7 / 9: the persistent loop over the Jones-vector path (32-bit cell words; 64-bit
+// cell words for scenes of more than 16 polygons).  Waves per SIMD: 5 for the full-colour
+// single-trace kernel over 32-bit cells (<= 96 VGPRs, no spills; 2 % faster than 4 on C3), 4 for
+// the others (<= 128 VGPRs: at 96 they spill).
 #ifndef WGRT_JONES_WAVES
-#define WGRT_JONES_WAVES 4         // waves per SIMD of the single-trace kernels (<= 128 VGPRs)
-#endif
-#ifndef WGRT_JONES_FUSED_WAVES
-#define WGRT_JONES_FUSED_WAVES 3   // ... of the fused ones (their hand-off state does not fit 128)
+#define WGRT_JONES_WAVES 5
 #endif
 template <class CellT, bool FUSED, bool SINGLE>
-__global__ __launch_bounds__(256, FUSED ? WGRT_JONES_FUSED_WAVES : WGRT_JONES_WAVES) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
+constexpr int jones_waves() {
+    return (sizeof(CellT) == 4 && !FUSED && !SINGLE) ? WGRT_JONES_WAVES : 4;
+}
+template <class CellT, bool FUSED, bool SINGLE>
+__global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
     jones_body<FUSED, SINGLE>(A, loc, counter, chunk);
 }
@@ -609,17 +612,23 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
     {
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
-        // resident workgroups of each instantiation (cell width x fused; the single-wavelength
-        // kernels have their full-colour twins' register budgets)
+        // resident workgroups of each instantiation (cell width x fused x single wavelength)
         auto grid_of = [&](const void *k, int &out) -> hipError_t {
             const hipError_t e = hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, k, 256, 0);
             out = std::max(1, cus * std::max(1, per_cu));
             return e;
         };
-        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint32_t, false, false>, s->jones_grid[0][0]));
-        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint32_t, true, false>, s->jones_grid[0][1]));
-        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint64_t, false, false>, s->jones_grid[1][0]));
-        HIP_TRY(grid_of((const void *)trace_jones_kernel<uint64_t, true, false>, s->jones_grid[1][1]));
+#define WGRT_GRID(CELL, C, F, S) \
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<CELL, F, S>, s->jones_grid[C][F][S]))
+        WGRT_GRID(uint32_t, 0, false, false);
+        WGRT_GRID(uint32_t, 0, false, true);
+        WGRT_GRID(uint32_t, 0, true, false);
+        WGRT_GRID(uint32_t, 0, true, true);
+        WGRT_GRID(uint64_t, 1, false, false);
+        WGRT_GRID(uint64_t, 1, false, true);
+        WGRT_GRID(uint64_t, 1, true, false);
+        WGRT_GRID(uint64_t, 1, true, true);
+#undef WGRT_GRID
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
@@ -829,7 +838,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         HIP_TRY(hipGetLastError());
         return WGRT_OK;
     }
-    int64_t grid = workgroups > 0 ? workgroups : s->jones_grid[variant == 9][num_iter > 1];
+    int64_t grid = workgroups > 0 ? workgroups : s->jones_grid[variant == 9][num_iter > 1][single];
     const int64_t useful = (n_rays + 255) / 256;
     if (grid > useful) grid = useful;
     wgrt_scene *ms = const_cast<wgrt_scene *>(s);
@@ -889,8 +898,10 @@ wgrt_status wgrt_scene_reserve(const wgrt_scene *s, int64_t n_rays, int num_iter
     if (!s) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene");
     if (n_rays < 0 || num_iter < 0 || num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "bad n_rays / num_iter");
     if (n_rays == 0) return WGRT_OK;
-    const int64_t grid = std::max(std::max(s->jones_grid[0][0], s->jones_grid[0][1]),
-                                  std::max(s->jones_grid[1][0], s->jones_grid[1][1]));
+    int64_t grid = 0;
+    for (int c = 0; c < 2; ++c)
+        for (int f = 0; f < 2; ++f)
+            for (int g = 0; g < 2; ++g) grid = std::max<int64_t>(grid, s->jones_grid[c][f][g]);
     wgrt_scene::Scratch *sc = nullptr;
     return ensure_scratch(const_cast<wgrt_scene *>(s), stream, n_rays, std::max(num_iter, 1),
                           std::min<int64_t>(grid, (n_rays + 255) / 256), &sc);
