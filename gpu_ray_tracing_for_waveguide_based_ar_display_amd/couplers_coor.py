@@ -28,6 +28,8 @@ from __future__ import annotations
 
 from dataclasses import dataclass, field
 
+import math
+
 import numpy as np
 from scipy.spatial import ConvexHull
 
@@ -230,10 +232,22 @@ def _slice_polygon(px, py, n_slices_design, half_width):
 # the design
 # ----------------------------------------------------------------------------
 
+_pow = np.frompyfunc(math.pow, 2, 1)
+
+
+def _sq(x):
+    """``x ** 2`` as the reference evaluates it: on numpy float64 *scalars* inside its loops, which
+    numpy computes with the C library's ``pow(x, 2.0)`` -- and this libm's pow rounds about 1 in
+    1,200 squares differently from ``x * x``, the array path numpy takes for ``array ** 2``.
+    Elementwise ``math.pow`` (the same libm call) keeps the tables bit-identical
+    (tests/test_geometry_golden.py)."""
+    return np.asarray(_pow(x, 2.0), dtype=np.float64)
+
+
 def _field_angles(fx, fy):
     """Polar / azimuth angle of a field point (CC:226-227)."""
     tx, ty = np.tan(fx), np.tan(fy)
-    return np.arctan(np.sqrt(tx ** 2 + ty ** 2)), np.arctan2(ty, tx)
+    return np.arctan(np.sqrt(_sq(tx) + _sq(ty))), np.arctan2(ty, tx)
 
 
 def _pupil_tangents(d, k0, th, ph, kg):
@@ -246,7 +260,7 @@ def _pupil_tangents(d, k0, th, ph, kg):
     ky_ic = ky + kgy_ic
     xc, yc = d.ic_center
     k1 = ky_ic / kx_ic
-    root = d.ic_radius * np.sqrt(1 + k1 ** 2)
+    root = d.ic_radius * np.sqrt(1 + _sq(k1))
     b11 = yc - k1 * xc + root
     b12 = yc - k1 * xc - root
     kx_fc = kx_ic + kgx_fc
@@ -281,15 +295,15 @@ def _eyebox_rects(d, th, ph):
 
 def _tir_phase(n_g, th):
     """delta_s - delta_p of a TIR bounce at polar angle ``th`` (CC:689-711)."""
-    root = np.sqrt(n_g ** 2 * np.sin(th) ** 2 - 1)
+    root = np.sqrt(n_g ** 2 * _sq(np.sin(th)) - 1)
     delta_s = 2 * np.arctan(root / (n_g * np.cos(th)))
     delta_p = 2 * np.arctan(n_g * root / np.cos(th))
     return delta_s - delta_p
 
 
 def _polar_after(k0, n_g, kx, ky):
-    kz = np.sqrt(k0 ** 2 * n_g ** 2 - kx ** 2 - ky ** 2)
-    return np.arctan(np.sqrt((kx ** 2 + ky ** 2) / kz ** 2)), np.arctan2(ky, kx)
+    kz = np.sqrt(_sq(k0) * n_g ** 2 - _sq(kx) - _sq(ky))
+    return np.arctan(np.sqrt((_sq(kx) + _sq(ky)) / _sq(kz))), np.arctan2(ky, kx)
 
 
 def design_geometry(num_FOV_x: int = 120, num_FOV_y: int = 80,

@@ -29,6 +29,7 @@ out-coupling (BASELINE config 5, deep-bounce stress).
 from __future__ import annotations
 
 import os
+import warnings
 
 import numpy as np
 
@@ -154,18 +155,31 @@ def synthetic_luts(geom, seed: int = 0, profile: str = "default", jitter: float 
                 lut_oc1=oc1, lut_oc2=oc2)
 
 
+class LUTPrecisionWarning(UserWarning):
+    """A LUT was given in single precision (complex64 / float32)."""
+
+
 def validate_luts(luts: dict, num_lmd: int, nx: int, ny: int, nfc: int, noc: int) -> dict:
     """Shape / dtype checks for a LUT set (real or synthetic); returns complex128 copies.
 
     Raises ``ValueError`` naming the first table that does not match the
     geometry (the reference indexes them without checks, MAIN:28-34).
+
+    Single-precision tables (complex64, as ``np.save`` of a complex64 array gives) are
+    accepted and widened exactly to complex128, with a :class:`LUTPrecisionWarning`: the
+    compiled reference kernel takes ``math.cos`` of a complex64 table's float32 ``.real``
+    (GRTF:866-869 and every cos ratio after it) in single precision, while the scene
+    builder here evaluates every cosine in double precision, so a draw lying within
+    float32 rounding of a branch threshold could be decided differently.  Parity with
+    the reference is pinned for complex128 tables only (the real files are not available
+    offline; their dtype is unknown).  The input dtypes are in ``validate_luts.last_dtypes``.
     """
     want = {"lut_ic1": (num_lmd, nx, ny), "lut_ic2": (num_lmd, nx, ny), "lut_ic3": (num_lmd, nx, ny),
             "lut_fc1": (nfc, num_lmd, nx, ny), "lut_fc2": (nfc, num_lmd, nx, ny),
             "lut_oc1": (noc, num_lmd, nx, ny), "lut_oc2": (noc, num_lmd, nx, ny)}
     min_ch = {"lut_ic1": 41, "lut_ic2": 32, "lut_ic3": 30, "lut_fc1": 19, "lut_fc2": 20,
               "lut_oc1": 39, "lut_oc2": 41}
-    out = {}
+    out, dtypes, single = {}, {}, []
     for name in LUT_NAMES:
         if name not in luts:
             raise ValueError(f"missing LUT {name}")
@@ -176,17 +190,36 @@ def validate_luts(luts: dict, num_lmd: int, nx: int, ny: int, nfc: int, noc: int
             raise ValueError(f"{name}: {a.shape[-1]} channels, kernel reads channel {min_ch[name] - 1}")
         if not (np.iscomplexobj(a) or np.issubdtype(a.dtype, np.floating)):
             raise ValueError(f"{name}: dtype {a.dtype} is not complex/real floating")
+        dtypes[name] = a.dtype
+        if a.dtype in (np.complex64, np.float32, np.float16):
+            single.append(name)
         out[name] = np.ascontiguousarray(a, dtype=np.complex128)
+    validate_luts.last_dtypes = dtypes
+    if single:
+        warnings.warn(f"single-precision LUTs {single} widened to complex128: parity with the reference "
+                      "is pinned for complex128 tables only (see validate_luts)", LUTPrecisionWarning, stacklevel=2)
     return out
 
 
+validate_luts.last_dtypes = {}
+
+
 def load_luts(directory: str = ".", suffix: str = "_fullColor.npy") -> dict:
-    """Load the seven reference LUT files (MAIN:28-34) with ``allow_pickle=False``."""
+    """Load the seven reference LUT files (MAIN:28-34) with ``allow_pickle=False``, dtypes as stored
+    (``validate_luts`` checks and widens them)."""
     luts = {}
     for name in LUT_NAMES:
         path = os.path.join(directory, name + suffix)
         luts[name] = np.load(path, allow_pickle=False)
     return luts
+
+
+def save_luts(luts: dict, directory: str, suffix: str = "_fullColor.npy", dtype=None) -> None:
+    """Write a LUT set as the reference's seven ``.npy`` files (``load_luts``'s inverse)."""
+    os.makedirs(directory, exist_ok=True)
+    for name in LUT_NAMES:
+        a = np.asarray(luts[name])
+        np.save(os.path.join(directory, name + suffix), a if dtype is None else a.astype(dtype))
 
 
 def single_wavelength(luts: dict, lut_TIR: np.ndarray, lut_gap: np.ndarray, l: int):

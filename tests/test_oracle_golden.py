@@ -67,3 +67,26 @@ def test_single_wavelength_threshold_is_pinned():
     eb = np.zeros(case.eb_shape(), np.float32)
     _, per_ray = sc.trace(case.rays, rng, eb, per_ray_bounces=True)
     assert (per_ray != case.f["bounces"][0]).sum() > 10
+
+
+def test_h6_fixture_exercises_eyebox_aliasing():
+    """h6_edge_rgb pins GRTF:154-165's compiled-numba addressing: its four crafted out-couplings
+    (gen_golden.craft_h6) land where only the aliasing puts them -- x == xmax on column 0 of the
+    next row, the on-edge band left of xmin on column 119, y == ymax on row 0 of the next FoV's
+    slab, the band below ymin on row 79 -- and each is counted after launch 1."""
+    case = GoldenCase("h6_edge_rgb")
+    ev = case.f["h6_events"]
+    assert sorted(ev[:, 0].tolist()) == [0, 1, 2, 3]
+    slab = case.ny * case.nx * 80 * 120
+    eb1 = case.eb_expected(1).reshape(-1)
+    for kind, gid, m, n, lam, off in ev:
+        assert eb1[lam * slab + off] >= 1
+        row, col, fov = (off // 120) % 80, off % 120, off // (80 * 120)
+        if kind == 0:
+            assert col == 0 and fov == n * case.nx + m
+        elif kind == 1:
+            assert col == 119 and fov == n * case.nx + m
+        elif kind == 2:
+            assert row == 0 and fov == n * case.nx + m + 1
+        else:
+            assert row == 79 and fov == n * case.nx + m
