@@ -104,6 +104,41 @@ def trace_job(shard: Shard, build_rays_fn, trace_fn, new_eb, num_iter: int = 4, 
     return reduce_eyebox(eb, group), rng
 
 
+def timed_run(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: int, stats, sync=None, hook=None,
+              group=None):
+    """bench.py's timed region on one rank: barrier + ``sync()``, ``steps`` chained traces of the
+    shard (``run_steps``), the eyebox reduce to rank 0, ``sync()`` + barrier.  ``stats[0]`` (the
+    device bounce counter, zeroed here) is what the tracer adds to.  Returns ``(elapsed, bounces,
+    bounces_local)``: the wall time MAX over ranks, the bounce total SUM over ranks, this rank's
+    own bounces.  The two small all-reduces run on ``stats``'s device (RCCL on the GPU box, gloo
+    in the CPU tests)."""
+    import time
+
+    import torch
+    import torch.distributed as dist
+    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    sync = sync or (lambda: None)
+    stats.zero_()
+    if multi:
+        dist.barrier(group)
+    sync()
+    t0 = time.perf_counter()
+    if steps and (rng.numel() if hasattr(rng, "numel") else len(rng)):
+        run_steps(trace_fn, rays, rng, eb, gid_offset, steps, per_call, hook)
+    reduce_eyebox(eb, group)
+    sync()
+    if multi:
+        dist.barrier(group)
+    elapsed = time.perf_counter() - t0
+    local = int(stats[0].item())
+    t = torch.tensor([elapsed], dtype=torch.float64, device=stats.device)
+    b = torch.tensor([local], dtype=torch.int64, device=stats.device)
+    if multi:
+        dist.all_reduce(t, op=dist.ReduceOp.MAX, group=group)
+        dist.all_reduce(b, op=dist.ReduceOp.SUM, group=group)
+    return float(t.item()), int(b.item()), local
+
+
 def hip_tracer(scene, variant: int = 0, stats=None):
     """trace_fn for ``run_steps`` / ``trace_job`` using the HIP kernel (torch device tensors);
     ``stats`` (int64[4] device tensor) is added to by every call."""
@@ -133,5 +168,5 @@ def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_l
     return rays, rng_seeds(rays["x"].shape[0], block_lo * rays_per_fov)
 
 
-__all__ = ["block_range", "Shard", "make_shard", "split_calls", "run_steps", "reduce_eyebox", "trace_job",
+__all__ = ["block_range", "Shard", "make_shard", "split_calls", "run_steps", "reduce_eyebox", "trace_job", "timed_run",
            "hip_tracer", "hip_shard_builder", "shard_rays_host", "MAX_TRACES_PER_CALL"]
