@@ -19,6 +19,7 @@ ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline", "wgrt_debug_set_cert_tol32",
+            "wgrt_debug_set_host_scene", "wgrt_debug_scene_copy",
             "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -136,6 +137,11 @@ def load(path: str = LIB_PATH):
     if hasattr(L, "wgrt_debug_set_timeline"):
         L.wgrt_debug_set_timeline.restype = None
         L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
+    if hasattr(L, "wgrt_debug_set_host_scene"):
+        L.wgrt_debug_set_host_scene.restype = ctypes.c_int
+        L.wgrt_debug_set_host_scene.argtypes = [ctypes.c_int]
+        L.wgrt_debug_scene_copy.restype = st
+        L.wgrt_debug_scene_copy.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int64]
     if hasattr(L, "wgrt_debug_set_cert_tol32"):
         L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
         L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]
@@ -265,6 +271,19 @@ class Scene:
         inf = SceneInfo()
         check(load().wgrt_scene_get_info(self.handle, ctypes.byref(inf)), "wgrt_scene_get_info")
         return {f: getattr(inf, f) for f, _ in SceneInfo._fields_}
+
+    def debug_copy(self, which: str) -> np.ndarray:
+        """Host copy of a device structure (wgrt_debug_scene_copy): "cells" (uint64 [ncy, ncx]),
+        "tiles" / "jtiles" (float64 [tiles, doubles per tile])."""
+        inf = self.info()
+        if which == "cells":
+            out = np.empty((inf["grid_cells_y"], inf["grid_cells_x"]), np.uint64)
+        else:
+            per = inf["tile_bytes" if which == "tiles" else "jtile_bytes"] // 8
+            out = np.empty((inf["tiles"], per), np.float64)
+        k = {"cells": 0, "tiles": 1, "jtiles": 2}[which]
+        check(load().wgrt_debug_scene_copy(self.handle, k, out.ctypes.data, out.nbytes), "wgrt_debug_scene_copy")
+        return out
 
     def eb_shape(self):
         if self.single_lambda:   # process_rays_kernel_pro's matrix_EB [NY, NX, 80, 120]

@@ -26,6 +26,7 @@ struct wgrt_scene {
     double *d_bands = nullptr;
     wgrt::LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
     int64_t tiles = 0;
+    int64_t edge_cells = 0;        // locator cells with an EDGE class
     int jones_grid[2][2][2] = {};   // resident 256-thread workgroups: [64-bit cells][fused][single wavelength]
     // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so
     // they may share it; launches on different streams never do)

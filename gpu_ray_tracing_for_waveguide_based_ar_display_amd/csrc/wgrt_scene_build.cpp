@@ -32,15 +32,13 @@
 #include <vector>
 
 #include "wgrt_common.h"
+#include "wgrt_pack.h"
 #include "wgrt_scene_build.h"
 #include "../../include/wgrt.h"
 
 namespace wgrt {
 
 namespace {
-
-constexpr double kPad = 1e-6;          // mm; >> tol (1e-12) and >> float64 rounding at |x| ~ 60 mm
-constexpr double kShortEdge = 1e-4;    // mm; shorter edges use the bbox criterion
 
 struct Poly {
     const double *xy;
@@ -78,8 +76,8 @@ void check(bool ok, const std::string &msg) {
 
 }  // namespace
 
-void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
-                   double cell_mm, LocatorHost &out) {
+void build_locator_geometry(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                            double cell_mm, LocatorHost &out) {
     const int np = (int)polys.size();
     check(np <= 32, "at most 32 polygons (eff_reg1, eff_reg2, IC, FC and OC slices) are supported");
     double xmin = INFINITY, xmax = -INFINITY, ymin = INFINITY, ymax = -INFINITY;
@@ -115,10 +113,8 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
     out.inv_h = 1.0 / h;
     out.ncx = ncx;
     out.ncy = ncy;
-    out.cells.assign((size_t)ncx * ncy, 0ull);
+    out.cells.clear();
     out.edge_cells = 0;
-
-    std::vector<uint8_t> edge((size_t)ncx * ncy);
     out.row_off.assign((size_t)np * ncy + 1, 0);
     out.row_edges.clear();
     for (int k = 0; k < np; ++k) {
@@ -156,42 +152,31 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
             }
         }
     }
+}
+
+void classify_cells_host(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                         LocatorHost &out) {
+    const int np = (int)polys.size();
+    const int ncx = out.ncx, ncy = out.ncy;
+    const double x0 = out.x0, y0 = out.y0, h = out.h;
+    out.cells.assign((size_t)ncx * ncy, 0ull);
+    out.edge_cells = 0;
+    std::vector<uint8_t> edge((size_t)ncx * ncy);
     std::vector<double> xs;
     for (int k = 0; k < np; ++k) {
         std::fill(edge.begin(), edge.end(), 0);
         const double *xy = polys[k];
         const int64_t nv = nverts[k];
-        const double pad2 = 2 * kPad;
-        // (1) EDGE cells, row by row: the cells of row cy (expanded by pad2) that the edge's
-        //     part inside the row's y-range (expanded by pad2) can reach, widened by pad2.
+        // (1) EDGE cells, row by row: the cells of row cy (expanded by 2 kPad) that the edge's
+        //     part inside the row's y-range (expanded by 2 kPad) can reach, widened by 2 kPad
+        //     (wgrt_pack.h edge_row_span, shared with the device build).
         for (int64_t i = 0, j = nv - 1; i < nv; j = i++) {
             const double ax = xy[2 * j], ay = xy[2 * j + 1], bx = xy[2 * i], by = xy[2 * i + 1];
-            const double len = std::hypot(bx - ax, by - ay);
-            const double ey0 = std::min(ay, by) - pad2, ey1 = std::max(ay, by) + pad2;
-            const int cy0 = std::max(0, (int)std::floor((ey0 - y0) / h) - 1);
-            const int cy1 = std::min(ncy - 1, (int)std::floor((ey1 - y0) / h) + 1);
+            int cy0, cy1;
+            edge_rows(ay, by, y0, h, ncy, cy0, cy1);
             for (int cy = cy0; cy <= cy1; ++cy) {
-                const double ry0 = y0 + cy * h - pad2, ry1 = y0 + (cy + 1) * h + pad2;
-                double lo, hi;
-                if (len < kShortEdge || std::fabs(by - ay) < 1e-300) {
-                    if (ey1 < ry0 || ey0 > ry1) continue;
-                    lo = std::min(ax, bx);
-                    hi = std::max(ax, bx);
-                } else {
-                    // parameter range of the segment inside [ry0, ry1]
-                    double t0 = (ry0 - ay) / (by - ay), t1 = (ry1 - ay) / (by - ay);
-                    if (t0 > t1) std::swap(t0, t1);
-                    t0 = std::max(t0, 0.0);
-                    t1 = std::min(t1, 1.0);
-                    if (t0 > t1 + 1e-12) continue;
-                    const double xa = ax + t0 * (bx - ax), xb = ax + t1 * (bx - ax);
-                    lo = std::min(xa, xb);
-                    hi = std::max(xa, xb);
-                }
-                lo -= pad2 + 1e-9;
-                hi += pad2 + 1e-9;
-                const int cx0 = std::max(0, (int)std::floor((lo - x0) / h));
-                const int cx1 = std::min(ncx - 1, (int)std::floor((hi - x0) / h));
+                int cx0, cx1;
+                if (!edge_row_span(ax, ay, bx, by, cy, x0, y0, h, ncx, cx0, cx1)) continue;
                 for (int cx = cx0; cx <= cx1; ++cx) edge[(size_t)cy * ncx + cx] = 1;
             }
         }
@@ -226,156 +211,66 @@ void build_locator(const std::vector<const double *> &polys, const std::vector<i
     }
 }
 
-namespace {
-
-struct LutView {
-    const double *p;  // complex interleaved
-    int64_t slices, L, nx, ny, ch;
-    const double *at(int64_t s, int64_t l, int64_t m, int64_t n, int64_t c) const {
-        return p + 2 * ((((s * L + l) * nx + m) * ny + n) * ch + c);
-    }
-};
-
-void put_rec(double *dst, const LutView &v, int64_t s, int64_t l, int64_t m, int64_t n, int p, int q,
-             int r, int t) {
-    const int ch[4] = {p, q, r, t};
-    for (int k = 0; k < 4; ++k) {
-        const double *c = v.at(s, l, m, n, ch[k]);
-        dst[2 * k] = c[0];
-        dst[2 * k + 1] = c[1];
-    }
+void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                   double cell_mm, LocatorHost &out) {
+    build_locator_geometry(polys, nverts, cell_mm, out);
+    classify_cells_host(polys, nverts, out);
 }
 
-}  // namespace
-
-void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles) {
-    const int64_t L = d.num_lmd, NX = d.nx, NY = d.ny;
-    const int nfc = (int)d.n_fc_slices, noc = (int)d.n_oc_slices;
-    const int TD = tile_doubles(nfc, noc);
-    tiles.assign((size_t)(L * NX * NY) * TD, 0.0);
-    const LutView ic1{d.lut_ic1, 1, L, NX, NY, d.ch5}, ic2{d.lut_ic2, 1, L, NX, NY, d.ch5},
-        ic3{d.lut_ic3, 1, L, NX, NY, d.ch5};
-    const LutView fc1{d.lut_fc1, nfc, L, NX, NY, d.ch3}, fc2{d.lut_fc2, nfc, L, NX, NY, d.ch3};
-    const LutView oc1{d.lut_oc1, noc, L, NX, NY, d.ch5}, oc2{d.lut_oc2, noc, L, NX, NY, d.ch5};
-    for (int64_t l = 0; l < L; ++l)
-        for (int64_t m = 0; m < NX; ++m)
-            for (int64_t n = 0; n < NY; ++n) {
-                double *T = tiles.data() + (size_t)((l * NX + m) * NY + n) * TD;
-                const int64_t g = (l * NX + m) * NY + n;
-                for (int k = 0; k < 4; ++k) {
-                    T[kTileTir + k] = d.lut_TIR[4 * g + k];
-                    T[kTileTirRot + 2 * k] = std::cos(d.lut_TIR[4 * g + k]);
-                    T[kTileTirRot + 2 * k + 1] = std::sin(d.lut_TIR[4 * g + k]);
-                }
-                for (int k = 0; k < 2; ++k) {
-                    T[kTileHopRot + 2 * k] = std::cos(2 * d.lut_TIR[4 * g + k]);
-                    T[kTileHopRot + 2 * k + 1] = std::sin(2 * d.lut_TIR[4 * g + k]);
-                }
-                for (int k = 0; k < 8; ++k) T[kTileGap + k] = d.lut_gap[8 * g + k];
-                const int64_t f = m * NY + n;
-                for (int k = 0; k < 4; ++k) T[kTileEbRange + k] = d.eff_reg_FOV_range[4 * f + k];
-                for (int k = 0; k < 8; ++k) T[kTileEbRect + k] = d.eff_reg_FOV[8 * f + k];
-                const double c_ic1 = std::cos(ic1.at(0, l, m, n, 0)[0]);
-                const double c_ic2 = std::cos(ic2.at(0, l, m, n, 0)[0]);
-                const double c_ic3 = std::cos(ic3.at(0, l, m, n, 0)[0]);
-                T[kTileCosIc1] = c_ic1;
-                auto block = [&](int b) { return T + kTileHeader + kBlock * b; };
-                // in-coupling event (GRTF:860-869)
-                double *B = block(0);
-                B[0] = c_ic2, B[1] = c_ic3;
-                put_rec(B + kBlockRec, ic1, 0, l, m, n, 13, 18, 33, 38);
-                put_rec(B + kBlockRec + 8, ic1, 0, l, m, n, 15, 20, 35, 40);
-                // R0 (GRTF:909-918)
-                B = block(1);
-                B[0] = c_ic2, B[1] = c_ic3;
-                put_rec(B + kBlockRec, ic2, 0, l, m, n, 4, 9, 24, 29);
-                put_rec(B + kBlockRec + 8, ic2, 0, l, m, n, 6, 11, 26, 31);
-                // R1 (GRTF:955-964) -- the reference's (2, 22, 7, 27) argument order kept
-                B = block(2);
-                B[0] = c_ic2, B[1] = c_ic3;
-                put_rec(B + kBlockRec, ic3, 0, l, m, n, 2, 22, 7, 27);
-                put_rec(B + kBlockRec + 8, ic3, 0, l, m, n, 4, 9, 24, 29);
-                for (int k = 0; k < nfc; ++k) {
-                    const double cf1 = std::cos(fc1.at(k, l, m, n, 0)[0]);
-                    const double cf2 = std::cos(fc2.at(k, l, m, n, 0)[0]);
-                    B = block(3 + k);  // R2 (GRTF:1007-1016)
-                    B[0] = cf1, B[1] = cf2;
-                    put_rec(B + kBlockRec, fc1, k, l, m, n, 3, 6, 15, 18);
-                    put_rec(B + kBlockRec + 8, fc1, k, l, m, n, 2, 5, 14, 17);
-                    B = block(3 + nfc + k);  // R3 (GRTF:1060-1069)
-                    B[0] = cf1, B[1] = cf2;
-                    put_rec(B + kBlockRec, fc2, k, l, m, n, 4, 7, 16, 19);
-                    put_rec(B + kBlockRec + 8, fc2, k, l, m, n, 3, 6, 15, 18);
-                }
-                for (int k = 0; k < noc; ++k) {
-                    const double co1 = std::cos(oc1.at(k, l, m, n, 0)[0]);
-                    const double co2 = std::cos(oc2.at(k, l, m, n, 0)[0]);
-                    B = block(3 + 2 * nfc + k);  // R4 (GRTF:1117-1131)
-                    B[0] = co1, B[1] = co2, B[2] = c_ic1;
-                    put_rec(B + kBlockRec, oc1, k, l, m, n, 4, 9, 24, 29);
-                    put_rec(B + kBlockRec + 8, oc1, k, l, m, n, 2, 7, 22, 27);
-                    put_rec(B + kBlockRec + 16, oc1, k, l, m, n, 13, 18, 33, 38);
-                    B = block(3 + 2 * nfc + noc + k);  // R5 (GRTF:1186-1200)
-                    B[0] = co1, B[1] = co2, B[2] = c_ic1;
-                    put_rec(B + kBlockRec, oc2, k, l, m, n, 6, 11, 26, 31);
-                    put_rec(B + kBlockRec + 8, oc2, k, l, m, n, 4, 9, 24, 29);
-                    put_rec(B + kBlockRec + 16, oc2, k, l, m, n, 15, 20, 35, 40);
-                }
-            }
+PackView pack_view(const wgrt_scene_desc &d, const double *trig) {
+    PackView v;
+    v.ic1 = d.lut_ic1, v.ic2 = d.lut_ic2, v.ic3 = d.lut_ic3;
+    v.fc1 = d.lut_fc1, v.fc2 = d.lut_fc2, v.oc1 = d.lut_oc1, v.oc2 = d.lut_oc2;
+    v.tir = d.lut_TIR, v.gap = d.lut_gap, v.fov = d.eff_reg_FOV, v.fovr = d.eff_reg_FOV_range;
+    v.trig = trig;
+    v.L = d.num_lmd, v.NX = d.nx, v.NY = d.ny;
+    v.ch5 = (int)d.ch5, v.ch3 = (int)d.ch3, v.nfc = (int)d.n_fc_slices, v.noc = (int)d.n_oc_slices;
+    v.n_g = d.n_g;
+    return v;
 }
 
-void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std::vector<double> &jt) {
-    const int64_t L = d.num_lmd, NX = d.nx, NY = d.ny;
+void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig) {
     const int nfc = (int)d.n_fc_slices, noc = (int)d.n_oc_slices;
-    const int TD = tile_doubles(nfc, noc), JD = jtile_doubles(nfc, noc);
-    const int nblk = 3 + 2 * nfc + 2 * noc;
-    jt.assign((size_t)(L * NX * NY) * JD, 0.0);
-    for (int64_t g = 0; g < L * NX * NY; ++g) {
-        const double *T = tiles.data() + (size_t)g * TD;
-        double *J = jt.data() + (size_t)g * JD;
-        const double *tir = d.lut_TIR + 4 * g;
-        for (int k = 0; k < 8; ++k) J[kJGap + k] = T[kTileGap + k];
-        for (int k = 0; k < 4; ++k) J[kJHop + k] = T[kTileHopRot + k];
-        J[kJCosIc1] = T[kTileCosIc1];
-        double tir_max = 0.0;
-        for (int k = 0; k < 4; ++k) tir_max = std::max(tir_max, std::fabs(tir[k]));
-        J[kJGrowth] = std::max(1.0, tir_max / kPi);
-        for (int b = 0; b < nblk; ++b) {
-            const double *B = T + kTileHeader + kBlock * b;
-            double *O = J + kJHeader + kJBlock * b;
-            const bool three = b >= 3 + 2 * nfc;
-            // TIR step of the taken branches (GRTF:877, 926, 942, 1026, 1039, ...): block 0-2 (IC
-            // states) TIR[0] / TIR[2], FC blocks TIR[0] / TIR[1], OC blocks TIR[1] / TIR[3]
-            const int ta = b < 3 ? 0 : (three ? 1 : 0), tb = b < 3 ? 2 : (three ? 3 : 1);
-            double sum = 0.0;
-            for (int k = 0; k < 3; ++k) {
-                O[kJBlockCos + k] = B[kBlockCos + k];
-                double *rec = O + kJBlockRec + 8 * k;
-                for (int j = 0; j < 8; ++j) rec[j] = B[kBlockRec + 8 * k + j];
-                double w = 0.0;
-                if (k < 2 || three) {
-                    const double p = std::hypot(rec[0], rec[1]), q = std::hypot(rec[2], rec[3]);
-                    const double r = std::hypot(rec[4], rec[5]), s = std::hypot(rec[6], rec[7]);
-                    const double f = (b == 0) ? d.n_g : (k == 2 ? 1.0 / d.n_g : 1.0);
-                    // 1.01: covers the rounding of this bound itself
-                    w = ((p + r) * (p + r) + (q + s) * (q + s)) * std::fabs(B[kBlockCos + k]) * f * 1.01;
-                }
-                if (k < 2) {   // turn the TM output row (q, s) by e^{i lut_TIR[t]}
-                    const double th = tir[k == 0 ? ta : tb], c = std::cos(th), sn = std::sin(th);
-                    for (int j : {2, 6}) {
-                        const double re = rec[j], im = rec[j + 1];
-                        rec[j] = re * c - im * sn;
-                        rec[j + 1] = re * sn + im * c;
-                    }
-                }
-                O[kJBlockW + k] = w;
-                sum += w;
-                float *r32 = (float *)(O + kJBlockRec32) + 8 * k;   // the estimate's single-precision copy
-                for (int j = 0; j < 8; ++j) r32[j] = (float)rec[j];
-            }
-            O[kJBlockWsum] = sum * 1.01;
+    const int TG = trig_doubles(nfc, noc);
+    const int64_t ntiles = (int64_t)d.num_lmd * d.nx * d.ny;
+    trig.assign((size_t)ntiles * TG, 0.0);
+    const PackView v = pack_view(d, nullptr);
+    for (int64_t g = 0; g < ntiles; ++g) {
+        const int64_t n = g % d.ny, m = g / d.ny % d.nx, l = g / ((int64_t)d.ny * d.nx);
+        double *t = trig.data() + (size_t)g * TG;
+        // math.cos of each LUT's polar angle (channel 0, real part; GRTF:868-1200)
+        t[0] = std::cos(lut_at(d.lut_ic1, 0, l, m, n, 0, v, v.ch5)[0]);
+        t[1] = std::cos(lut_at(d.lut_ic2, 0, l, m, n, 0, v, v.ch5)[0]);
+        t[2] = std::cos(lut_at(d.lut_ic3, 0, l, m, n, 0, v, v.ch5)[0]);
+        for (int k = 0; k < nfc; ++k) {
+            t[3 + k] = std::cos(lut_at(d.lut_fc1, k, l, m, n, 0, v, v.ch3)[0]);
+            t[3 + nfc + k] = std::cos(lut_at(d.lut_fc2, k, l, m, n, 0, v, v.ch3)[0]);
+        }
+        for (int k = 0; k < noc; ++k) {
+            t[3 + 2 * nfc + k] = std::cos(lut_at(d.lut_oc1, k, l, m, n, 0, v, v.ch5)[0]);
+            t[3 + 2 * nfc + noc + k] = std::cos(lut_at(d.lut_oc2, k, l, m, n, 0, v, v.ch5)[0]);
+        }
+        double *rot = t + 3 + 2 * nfc + 2 * noc;
+        for (int k = 0; k < 4; ++k) {
+            rot[2 * k] = std::cos(d.lut_TIR[4 * g + k]);
+            rot[2 * k + 1] = std::sin(d.lut_TIR[4 * g + k]);
+        }
+        for (int k = 0; k < 2; ++k) {
+            rot[8 + 2 * k] = std::cos(2 * d.lut_TIR[4 * g + k]);
+            rot[8 + 2 * k + 1] = std::sin(2 * d.lut_TIR[4 * g + k]);
         }
     }
+}
+
+void pack_tiles_host(const wgrt_scene_desc &d, const std::vector<double> &trig, std::vector<double> &tiles,
+                     std::vector<double> &jtiles) {
+    const int nfc = (int)d.n_fc_slices, noc = (int)d.n_oc_slices;
+    const int TD = tile_doubles(nfc, noc), JD = jtile_doubles(nfc, noc);
+    const int64_t ntiles = (int64_t)d.num_lmd * d.nx * d.ny;
+    tiles.assign((size_t)ntiles * TD, 0.0);
+    jtiles.assign((size_t)ntiles * JD, 0.0);
+    const PackView v = pack_view(d, trig.data());
+    for (int64_t g = 0; g < ntiles; ++g) pack_tile(v, g, tiles.data() + (size_t)g * TD, jtiles.data() + (size_t)g * JD);
 }
 
 void validate_desc(const wgrt_scene_desc &d) {
@@ -397,10 +292,9 @@ void validate_desc(const wgrt_scene_desc &d) {
     check(d.n_oc_slices == 0 || d.OC_offset[0] >= 0, "OC_offset[0] < 0");
 }
 
-void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) {
-    validate_desc(d);
-    std::vector<const double *> polys;
-    std::vector<int64_t> nv;
+void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys, std::vector<int64_t> &nv) {
+    polys.clear();
+    nv.clear();
     polys.push_back(d.eff_reg1);
     nv.push_back(d.n_eff_reg1);
     polys.push_back(d.eff_reg2);
@@ -415,12 +309,25 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out) 
         polys.push_back(d.OC + 2 * d.OC_offset[k]);
         nv.push_back(d.OC_offset[k + 1] - d.OC_offset[k]);
     }
-    build_locator(polys, nv, cell_mm, out.loc);
-    pack_tiles(d, out.tiles);
-    pack_jtiles(d, out.tiles, out.jtiles);
-    // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would
-    // make the reference's efficiencies NaN); such LUTs are rejected instead.
-    for (const double v : out.tiles) check(std::isfinite(v), "non-finite value in the LUTs / lut_TIR / lut_gap / eyebox tables");
+}
+
+void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells, bool pack) {
+    validate_desc(d);
+    std::vector<const double *> polys;
+    std::vector<int64_t> nv;
+    scene_polygons(d, polys, nv);
+    if (cells)
+        build_locator(polys, nv, cell_mm, out.loc);
+    else
+        build_locator_geometry(polys, nv, cell_mm, out.loc);
+    build_trig(d, out.trig);
+    if (pack) {
+        pack_tiles_host(d, out.trig, out.tiles, out.jtiles);
+        // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would
+        // make the reference's efficiencies NaN); such LUTs are rejected instead.
+        for (const double v : out.tiles)
+            check(std::isfinite(v), "non-finite value in the LUTs / lut_TIR / lut_gap / eyebox tables");
+    }
     out.tile_doubles = tile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
     out.jtile_doubles = jtile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
 }

@@ -5,6 +5,7 @@
 #include <vector>
 
 #include "../../include/wgrt.h"
+#include "wgrt_pack.h"
 
 namespace wgrt {
 
@@ -35,13 +36,25 @@ struct SceneHost {
     int tile_doubles = 0;
     std::vector<double> jtiles;    // [num_lmd * nx * ny][jtile_doubles] (Jones-vector variants)
     int jtile_doubles = 0;
+    std::vector<double> trig;      // [num_lmd * nx * ny][trig_doubles]: host-libm cos / sin (build_trig)
 };
 
+// grid extent, vertices, row-band edge lists and band records (everything but the cell words)
+void build_locator_geometry(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                            double cell_mm, LocatorHost &out);
+// the cell words on the host (the device builds them with the same edge_row_span / parity rules)
+void classify_cells_host(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
+                         LocatorHost &out);
 void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
                    double cell_mm, LocatorHost &out);
-void pack_tiles(const wgrt_scene_desc &d, std::vector<double> &tiles);
-void pack_jtiles(const wgrt_scene_desc &d, const std::vector<double> &tiles, std::vector<double> &jtiles);
+PackView pack_view(const wgrt_scene_desc &d, const double *trig);
+void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig);
+void pack_tiles_host(const wgrt_scene_desc &d, const std::vector<double> &trig, std::vector<double> &tiles,
+                     std::vector<double> &jtiles);
 void validate_desc(const wgrt_scene_desc &d);
-void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out);
+// cells: classify the grid on the host; pack: pack the tiles on the host
+void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells = true, bool pack = true);
+// the polygon list the locator covers: eff_reg1, eff_reg2, IC, FC slices, OC slices
+void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys, std::vector<int64_t> &nv);
 
 }  // namespace wgrt

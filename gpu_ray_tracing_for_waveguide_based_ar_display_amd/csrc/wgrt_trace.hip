@@ -551,9 +551,111 @@ __global__ __launch_bounds__(256) void selftest_math_kernel(const double *a, con
     out[6 * n + i] = wrap_pi(x);
 }
 
+// ---------------------------------------------------------------------------------------------
+// Scene build on the device (wgrt_scene_create): the locator's cell words and the LUT tiles.
+// ---------------------------------------------------------------------------------------------
+// EDGE marks: one thread per (polygon edge, grid row); the row's cells the edge reaches get the
+// polygon's bit (wgrt_pack.h edge_row_span, the host build's rule).
+__global__ __launch_bounds__(256) void edge_mark_kernel(const double *verts, const int32_t *poly_off, int npoly,
+                                                        double x0, double y0, double h, int ncx, int ncy,
+                                                        uint32_t *mask) {
+    const int e = blockIdx.y;   // global edge index: polygon k's edge (i - 1 -> i), i = e - poly_off[k]
+    int k = 0;
+    while (k + 1 < npoly && poly_off[k + 1] <= e) ++k;
+    const int a = poly_off[k], nv = poly_off[k + 1] - a, i = e - a;
+    if (nv <= 0 || i < 0 || i >= nv) return;
+    const int j = i == 0 ? nv - 1 : i - 1;
+    const double ax = verts[2 * (a + j)], ay = verts[2 * (a + j) + 1];
+    const double bx = verts[2 * (a + i)], by = verts[2 * (a + i) + 1];
+    int cy0, cy1;
+    edge_rows(ay, by, y0, h, ncy, cy0, cy1);
+    const int cy = cy0 + (int)(blockIdx.x * blockDim.x + threadIdx.x);
+    if (cy > cy1) return;
+    int cx0, cx1;
+    if (!edge_row_span(ax, ay, bx, by, cy, x0, y0, h, ncx, cx0, cx1)) return;
+    for (int cx = cx0; cx <= cx1; ++cx) atomicOr(mask + (size_t)cy * ncx + cx, 1u << k);
+}
+
+// Cell words: EDGE where marked, else the reference predicate's crossing parity at the cell
+// centre over the row's edges (every edge crossing the row's centre line is in its band list).
+__global__ __launch_bounds__(256) void classify_cells_kernel(const double *verts, const int32_t *poly_off, int npoly,
+                                                             const int32_t *row_off, const int32_t *row_edges,
+                                                             double x0, double y0, double h, int ncx, int ncy,
+                                                             const uint32_t *mask, uint64_t *cells, uint32_t *cells32,
+                                                             unsigned long long *edge_cells) {
+    const int64_t c = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    uint64_t edges = 0;
+    if (c < (int64_t)ncx * ncy) {
+        const int cy = (int)(c / ncx), cx = (int)(c % ncx);
+        const double px = x0 + (cx + 0.5) * h, py = y0 + (cy + 0.5) * h;
+        const uint32_t mk = mask[c];
+        uint64_t w = 0;
+        for (int k = 0; k < npoly; ++k) {
+            uint64_t cls;
+            if ((mk >> k) & 1u) {
+                cls = 2;
+                ++edges;
+            } else {
+                const int a = poly_off[k], nv = poly_off[k + 1] - a;
+                const int r = k * ncy + cy;
+                unsigned cnt = 0;
+                for (int e = row_off[r]; e < row_off[r + 1]; ++e) {
+                    const int i = row_edges[e], j = i == 0 ? nv - 1 : i - 1;
+                    const double xi = verts[2 * (a + i)], yi = verts[2 * (a + i) + 1];
+                    const double xj = verts[2 * (a + j)], yj = verts[2 * (a + j) + 1];
+                    if ((yi > py) != (yj > py)) cnt += px < (xj - xi) * (py - yi) / (yj - yi + 1e-20) + xi;
+                }
+                cls = cnt & 1u;
+            }
+            w |= cls << (2 * k);
+        }
+        cells[c] = w;
+        if (cells32) cells32[c] = (uint32_t)w;
+    }
+    edges = wave_sum(edges);
+    if ((threadIdx.x & 63) == 0 && edges) atomicAdd(edge_cells, (unsigned long long)edges);
+}
+
+// One thread per (lambda, m, n) tile: the exact lane's tile and its Jones-vector tile
+// (wgrt_pack.h pack_tile, the host build's code); flags any non-finite value.
+__global__ __launch_bounds__(64) void pack_tiles_kernel(PackView v, int64_t ntiles, double *tiles, double *jtiles,
+                                                        int td, int jd, int *nonfinite) {
+    const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (g >= ntiles) return;
+    double *T = tiles + g * td;
+    pack_tile(v, g, T, jtiles + g * jd);
+    bool bad = false;
+    for (int k = 0; k < td; ++k) bad |= !isfinite(T[k]);
+    if (bad) atomicOr(nonfinite, 1);
+}
+
 }  // namespace
 
 namespace {
+
+bool g_host_scene = [] {   // wgrt_debug_set_host_scene / env WGRT_SCENE_HOST=1: build scenes on the host
+    const char *v = getenv("WGRT_SCENE_HOST");
+    return v && atoi(v) != 0;
+}();
+
+// hipMalloc + copy of n elements (n may be 0)
+template <class T>
+wgrt_status upload_n(const T *src, size_t n, T **dst) {
+    const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+    hipError_t e = hipMalloc((void **)dst, bytes);
+    if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc: out of memory");
+    if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    if (n) HIP_TRY(hipMemcpy(*dst, src, n * sizeof(T), hipMemcpyHostToDevice));
+    return WGRT_OK;
+}
+
+template <class T>
+wgrt_status alloc_n(size_t n, T **dst) {
+    hipError_t e = hipMalloc((void **)dst, std::max<size_t>(n, 1) * sizeof(T));
+    if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc: out of memory");
+    if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc: ") + hipGetErrorString(e));
+    return WGRT_OK;
+}
 
 template <class T>
 wgrt_status upload(const std::vector<T> &v, T **dst) {
@@ -572,42 +674,119 @@ extern "C" {
 wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scene **out) {
     if (!desc || !out) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL desc / out");
     *out = nullptr;
+    const wgrt_scene_desc &d = *desc;
+    // host: validation, the locator's geometry (extent, vertices, row bands) and the trig table
+    // (every cos / sin on the host libm); the cell words and the tiles are built on the device
+    // (wgrt_debug_set_host_scene: both on the host, the reference build the device one is
+    // checked against)
     SceneHost host;
     try {
-        build_scene_host(*desc, g_cell_mm, host);
+        build_scene_host(d, g_cell_mm, host, g_host_scene, g_host_scene);
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
     HIP_TRY(hipSetDevice(device));
     auto *s = new wgrt_scene();
     s->device = device;
-    s->nx = desc->nx;
-    s->ny = desc->ny;
-    s->nl = desc->num_lmd;
-    s->nfc = (int)desc->n_fc_slices;
-    s->noc = (int)desc->n_oc_slices;
+    s->nx = d.nx;
+    s->ny = d.ny;
+    s->nl = d.num_lmd;
+    s->nfc = (int)d.n_fc_slices;
+    s->noc = (int)d.n_oc_slices;
     s->tile_d = host.tile_doubles;
     s->jtile_d = host.jtile_doubles;
     s->npoly = 3 + s->nfc + s->noc;
-    s->n_g = desc->n_g;
+    s->n_g = d.n_g;
     s->tiles = (int64_t)s->nl * s->nx * s->ny;
     wgrt_status st;
-    if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.jtiles, &s->d_jtiles)) != WGRT_OK ||
-        (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK ||
-        (st = upload(host.loc.verts, &s->d_verts)) != WGRT_OK ||
+    auto bail = [&](wgrt_status e) {
+        wgrt_scene_destroy(s);
+        return e;
+    };
+    if ((st = upload(host.loc.verts, &s->d_verts)) != WGRT_OK ||
         (st = upload(host.loc.poly_off, &s->d_poly_off)) != WGRT_OK ||
         (st = upload(host.loc.row_off, &s->d_row_off)) != WGRT_OK ||
         (st = upload(host.loc.row_edges, &s->d_row_edges)) != WGRT_OK ||
-        (st = upload(host.loc.bands, &s->d_bands)) != WGRT_OK) {
-        wgrt_scene_destroy(s);
-        return st;
-    }
-    if (s->npoly <= 16) {
-        std::vector<uint32_t> c32(host.loc.cells.begin(), host.loc.cells.end());
-        if ((st = upload(c32, &s->d_cells32)) != WGRT_OK) {
-            wgrt_scene_destroy(s);
-            return st;
+        (st = upload(host.loc.bands, &s->d_bands)) != WGRT_OK)
+        return bail(st);
+    const size_t ncells = (size_t)host.loc.ncx * host.loc.ncy;
+    if (g_host_scene) {
+        if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.jtiles, &s->d_jtiles)) != WGRT_OK ||
+            (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK)
+            return bail(st);
+        if (s->npoly <= 16) {
+            const std::vector<uint32_t> c32(host.loc.cells.begin(), host.loc.cells.end());
+            if ((st = upload(c32, &s->d_cells32)) != WGRT_OK) return bail(st);
         }
+        s->edge_cells = host.loc.edge_cells;
+    } else {
+        // the raw arrays the tiles are packed from, on the device for the packing only
+        const int64_t g = (int64_t)d.num_lmd * d.nx * d.ny, nfc = d.n_fc_slices, noc = d.n_oc_slices;
+        const size_t n5 = (size_t)g * d.ch5 * 2, n3 = (size_t)g * d.ch3 * 2;
+        double *raw[12] = {};
+        auto free_raw = [&]() {
+            for (double *p : raw) (void)hipFree(p);
+        };
+        const double *src[12] = {d.lut_ic1, d.lut_ic2, d.lut_ic3, d.lut_fc1, d.lut_fc2, d.lut_oc1, d.lut_oc2,
+                                 d.lut_TIR, d.lut_gap, d.eff_reg_FOV, d.eff_reg_FOV_range, host.trig.data()};
+        const size_t cnt[12] = {n5, n5, n5, nfc * n3, nfc * n3, noc * n5, noc * n5, (size_t)g * 4, (size_t)g * 8,
+                                (size_t)d.nx * d.ny * 8, (size_t)d.nx * d.ny * 4, host.trig.size()};
+        for (int k = 0; k < 12; ++k)
+            if ((st = upload_n(cnt[k] ? src[k] : nullptr, cnt[k], &raw[k])) != WGRT_OK) {
+                free_raw();
+                return bail(st);
+            }
+        PackView v = pack_view(d, raw[11]);
+        v.ic1 = raw[0], v.ic2 = raw[1], v.ic3 = raw[2], v.fc1 = raw[3], v.fc2 = raw[4], v.oc1 = raw[5], v.oc2 = raw[6];
+        v.tir = raw[7], v.gap = raw[8], v.fov = raw[9], v.fovr = raw[10];
+        int *flag = nullptr;
+        unsigned long long *ecount = nullptr;
+        uint32_t *mask = nullptr;
+        auto free_tmp = [&]() {
+            free_raw();
+            (void)hipFree(flag);
+            (void)hipFree(ecount);
+            (void)hipFree(mask);
+        };
+        if ((st = alloc_n((size_t)g * s->tile_d, &s->d_tiles)) != WGRT_OK ||
+            (st = alloc_n((size_t)g * s->jtile_d, &s->d_jtiles)) != WGRT_OK || (st = alloc_n(1, &flag)) != WGRT_OK ||
+            (st = alloc_n(1, &ecount)) != WGRT_OK || (st = alloc_n(ncells, &mask)) != WGRT_OK ||
+            (st = alloc_n(ncells, &s->d_cells)) != WGRT_OK ||
+            (s->npoly <= 16 && (st = alloc_n(ncells, &s->d_cells32)) != WGRT_OK)) {
+            free_tmp();
+            return bail(st);
+        }
+        HIP_TRY(hipMemset(s->d_tiles, 0, (size_t)g * s->tile_d * sizeof(double)));
+        HIP_TRY(hipMemset(s->d_jtiles, 0, (size_t)g * s->jtile_d * sizeof(double)));
+        HIP_TRY(hipMemset(flag, 0, sizeof(int)));
+        HIP_TRY(hipMemset(ecount, 0, sizeof(unsigned long long)));
+        HIP_TRY(hipMemset(mask, 0, ncells * sizeof(uint32_t)));
+        hipLaunchKernelGGL(pack_tiles_kernel, dim3((unsigned)((g + 63) / 64)), dim3(64), 0, 0, v, g, s->d_tiles,
+                           s->d_jtiles, s->tile_d, s->jtile_d, flag);
+        HIP_TRY(hipGetLastError());
+        const LocatorHost &L = host.loc;
+        const int npoly = (int)L.poly_off.size() - 1, n_edges = L.poly_off.back();
+        if (n_edges > 0) {
+            hipLaunchKernelGGL(edge_mark_kernel, dim3((unsigned)((L.ncy + 255) / 256), (unsigned)n_edges), dim3(256),
+                               0, 0, s->d_verts, s->d_poly_off, npoly, L.x0, L.y0, L.h, L.ncx, L.ncy, mask);
+            HIP_TRY(hipGetLastError());
+        }
+        hipLaunchKernelGGL(classify_cells_kernel, dim3((unsigned)((ncells + 255) / 256)), dim3(256), 0, 0, s->d_verts,
+                           s->d_poly_off, npoly, s->d_row_off, s->d_row_edges, L.x0, L.y0, L.h, L.ncx, L.ncy, mask,
+                           s->d_cells, s->d_cells32, ecount);
+        HIP_TRY(hipGetLastError());
+        int bad = 0;
+        unsigned long long ec = 0;
+        HIP_TRY(hipMemcpy(&bad, flag, sizeof(int), hipMemcpyDeviceToHost));
+        HIP_TRY(hipMemcpy(&ec, ecount, sizeof(ec), hipMemcpyDeviceToHost));
+        free_tmp();
+        if (bad) {
+            // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient
+            // would make the reference's efficiencies NaN); such LUTs are rejected instead.
+            return bail(fail(WGRT_ERR_INVALID_ARGUMENT,
+                             "non-finite value in the LUTs / lut_TIR / lut_gap / eyebox tables"));
+        }
+        s->edge_cells = (int64_t)ec;
     }
     {
         int cus = 0, per_cu = 0;
@@ -672,7 +851,7 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->grid_cells_x = s->loc_host.ncx;
     info->grid_cells_y = s->loc_host.ncy;
     info->grid_cell_mm = s->loc_host.h;
-    info->grid_edge_cells = s->loc_host.edge_cells;
+    info->grid_edge_cells = s->edge_cells;
     info->n_polygons = s->npoly;
     info->device = s->device;
     info->jtile_bytes = (int64_t)s->jtile_d * 8;
@@ -1039,6 +1218,29 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
         }
         out_mask[i] = mask;
     }
+    return WGRT_OK;
+}
+
+int wgrt_debug_set_host_scene(int on) {
+    const int prev = g_host_scene ? 1 : 0;
+    g_host_scene = on != 0;
+    return prev;
+}
+
+wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int64_t bytes) {
+    if (!s || !dst) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / dst");
+    const size_t ncells = (size_t)s->loc_host.ncx * s->loc_host.ncy;
+    const void *src = nullptr;
+    size_t n = 0;
+    switch (which) {
+        case 0: src = s->d_cells, n = ncells * sizeof(uint64_t); break;
+        case 1: src = s->d_tiles, n = (size_t)s->tiles * s->tile_d * sizeof(double); break;
+        case 2: src = s->d_jtiles, n = (size_t)s->tiles * s->jtile_d * sizeof(double); break;
+        default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles");
+    }
+    if (bytes != (int64_t)n) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes must be " + std::to_string(n));
+    HIP_TRY(hipSetDevice(s->device));
+    HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return WGRT_OK;
 }
 

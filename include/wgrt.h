@@ -269,6 +269,16 @@ wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, in
  * buf = NULL or n_waves = 0 turns it off (the default). */
 void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves);
 
+/* Debug hook (process-wide): scenes created while set are built entirely on the host (cell
+ * words and tiles by the same rules, host code) instead of on the device; returns the previous
+ * setting.  The host build is the reference the device build is checked against. */
+int wgrt_debug_set_host_scene(int on);
+
+/* Test hook: copies one of a scene's device structures to host memory dst (bytes must equal its
+ * size): which = 0 the locator cell words (uint64, ncx * ncy), 1 the exact lane's tiles,
+ * 2 the Jones-vector tiles (doubles, tiles * tile / jtile doubles; wgrt_scene_info). */
+wgrt_status wgrt_debug_scene_copy(const wgrt_scene *scene, int which, void *dst, int64_t bytes);
+
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */
 wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, double *out, void *stream);
