@@ -202,8 +202,8 @@ def kernel_name(variant, scene):
     when the scene has <= 16 polygons, else 9)."""
     if variant == 0:
         variant = 7 if scene.info()["n_polygons"] <= 16 else 9
-    return {1: "trace_grid_kernel", 7: "trace_jones_kernel<unsigned int, false>",
-            9: "trace_jones_kernel<unsigned long, false>"}[variant]
+    return {1: "trace_grid_kernel", 7: "trace_jones_kernel<unsigned int, false, false>",
+            9: "trace_jones_kernel<unsigned long, false, false>"}[variant]
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):
