@@ -189,6 +189,7 @@ __global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilog
 // of consecutive chunks (FoV x wavelength tiles stay in that XCD's L2) and the dequeue
 // atomics spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The
 // XCD id steers placement only: any wave may take any chunk, so correctness never depends on it.
+constexpr int kFusedRefill = 16;
 constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
                                // out-couples ~10 rays per trace; unused slots cost the eyebox
                                // epilogue a read each)
@@ -331,6 +332,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             }
         }
         uint64_t need = __ballot(!active && !waiting);
+        // fused launches refill in batches of kFusedRefill free lanes (or when the wave is empty):
+        // a refill's column loads are one round trip the whole wave waits for, and in a fused
+        // launch idle lanes are cheap (the next trace's rays keep the chip full): -4 % per trace
+        // on C3; single-trace launches gained nothing measurable from batching
+        if (FUSED && __popcll(need) < kFusedRefill && __ballot(active || waiting) != 0ull) need = 0ull;
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
                 // the dequeue for this item was issued when the previous one started (pend_v,
