@@ -185,11 +185,12 @@ __global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilog
 }
 
 // Work queue of the Jones-vector variants: one head per XCD (each on its own 128-B line), head
-// x handing out chunks [x n / 8, (x + 1) n / 8) in order, so a die's waves share one stretch
-// of consecutive chunks (FoV x wavelength tiles stay in that XCD's L2) and the dequeue
-// atomics spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The
-// XCD id steers placement only: any wave may take any chunk, so correctness never depends on it.
+// x handing out the stripes s = x, x + 8, ... of kStripe consecutive chunks, in order, so a
+// die's waves share its stripes' FoV x wavelength tiles in that XCD's L2 and the dequeue atomics
+// spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The XCD id
+// steers placement only: any wave may take any chunk, so correctness never depends on it.
 constexpr int kFusedRefill = 16;
+constexpr int64_t kStripe = 16;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
 constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
                                // out-couples ~10 rays per trace; unused slots cost the eyebox
                                // epilogue a read each)
@@ -251,11 +252,20 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
 
     // head x's items: iteration-major over its chunk range [lo, hi)
+    // head x's items: stripes of kStripe consecutive chunks, stripe s on head s % 8, iteration-
+    // major.  Every die gets a mix of all FoVs and wavelengths -- ray lifetimes differ by tile,
+    // and with one contiguous eighth of the tiles per head the die holding the long-lived tiles
+    // ended the launch 60 us after the first (striping: -6 % per single launch on C3) -- while
+    // a stripe's rays still share their tiles in that die's L2.
+    const int64_t ns = (n_chunks + kStripe - 1) / kStripe, last = n_chunks - (ns - 1) * kStripe;
     auto decode = [&](int x, int64_t q, int64_t &c, uint32_t &k) -> bool {
-        const int64_t lo = n_chunks * x / kHeads, hi = n_chunks * (x + 1) / kHeads, cx = hi - lo;
-        if (cx <= 0 || q >= cx * n_iter) return false;
+        if (x >= ns) return false;
+        int64_t cx = ((ns - x + kHeads - 1) / kHeads) * kStripe;
+        if ((ns - 1) % kHeads == x) cx -= kStripe - last;
+        if (q >= cx * n_iter) return false;
         k = (uint32_t)(q / cx);
-        c = lo + q % cx;
+        const int64_t r = q % cx;
+        c = ((r / kStripe) * kHeads + x) * kStripe + r % kStripe;
         return true;
     };
     // start the trace (L.i, L.k) on this lane: active, waiting (previous trace still running) or
