@@ -58,12 +58,14 @@ struct TraceArgs {
     double cert_tol32; // ... and of the single-precision estimate's bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
-    // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -}
-    // (trace-kernel workgroups first, then one slot per epilogue workgroup), summed into *stats by
-    // the finalize kernel -- no contended atomics on the four stats words
+    // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -} of
+    // the trace kernel, summed into *stats by the epilogue -- no contended atomics on the stats
     unsigned long long *part;
     int n_trace_waves;                  // partial slots of the trace kernel (one per workgroup)
-    unsigned long long *heads0;         // the launch scratch counters (kScratchCtr words)
+    unsigned long long *heads0;         // this launch's counter set (kScratchCtr words)
+    unsigned long long *other_ctr;      // the next launch's counter set, zeroed by this launch's epilogue
+    uint32_t *full_list;                // out-coupling queue blocks the trace waves filled (block numbers)
+    unsigned long long *full_count;
     unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_set_timeline), NULL normally
     int64_t timeline_waves;
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one

@@ -31,7 +31,11 @@ struct wgrt_scene {
     // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so
     // they may share it; launches on different streams never do)
     struct Scratch {
-        unsigned long long *ctr = nullptr;   // kHeads chunk heads (kHeadStride apart), replay count, queue count
+        // two counter sets (kHeads chunk heads kHeadStride apart, replay count, queue count,
+        // full-block count), used by alternate launches: a launch's epilogue zeroes the other one
+        unsigned long long *ctr = nullptr;
+        uint32_t parity = 0;                 // the set the next launch uses
+        uint32_t *full = nullptr;            // full-block list (qcap / kQBlock entries)
         uint32_t *list = nullptr;            // replay list
         int64_t cap = 0;                     // replay list entries
         double2 *q_xy = nullptr;             // out-coupling queue: position, ray index

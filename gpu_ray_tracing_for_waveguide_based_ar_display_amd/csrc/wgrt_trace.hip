@@ -88,32 +88,37 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 // count and the out-coupling queue count, each on its own 128-B line.
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
-constexpr int kScratchCtr = (kHeads + 2) * kHeadStride;   // heads, replay count, queue count
-constexpr int kScratchCtrWords = kScratchCtr;
+constexpr int kScratchCtr = (kHeads + 3) * kHeadStride;   // heads, replay / queue / full-block counts
 
-// Runs right behind every Jones-vector launch on its stream:
-//  1. bins the queued out-couplings (entry j: position q_xy[j], tile index q_i[j]) into
-//     matrix_EB -- the eyebox predicate, its divisions and the atomics stay out of the bounce
-//     loop; cells count hits (+1.0f), so the binning order does not matter;
+// Runs right behind every Jones-vector launch on its stream -- the launch's only other kernel:
+//  1. bins the out-coupling queue blocks the trace waves filled (a wave bins the block it holds
+//     when it leaves; cells count hits, +1.0f, so the binning order does not matter);
 //  2. re-traces the rays the launch abandoned (uncertain decisions; nothing of them was written)
 //     from their launch-start state with the reference arithmetic (usually none);
-//  3. stores its workgroup's counters in its partial slot (plain stores: finalize_kernel, the
-//     next kernel on the stream, sums them -- no contended atomics, no device-scope fences).
+//  3. adds the counters to *stats: workgroup 0 sums the trace kernel's per-workgroup partials,
+//     any workgroup with replay or binning work adds its own (rare, so the atomics are not
+//     contended);
+//  4. zeroes the other counter set, which the next launch on the stream uses (this launch's set
+//     is still being read by the other workgroups; the launch after next finds it zeroed).
 constexpr int kEpilogueGroups = 256;
+constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
+                               // out-couples ~10 rays per trace)
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     __shared__ unsigned long long red[4][3];
-    const unsigned long long nq = *A.q_count, nr = *A.replay_count;
+    const unsigned long long nr = *A.replay_count, nf = *A.full_count;
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
     uint64_t h = 0, b = 0, bad = 0;
-    for (unsigned long long j = tid; j < nq; j += nth) {
-        const uint32_t g = A.q_i[j];   // tile index (lambda * nx + m) * ny + n
-        const double2 p = A.q_xy[j];
-        if (g == 0xffffffffu) continue;   // a slot its wave left unused
-        const int n = (int)(g % (uint32_t)A.ny), m = (int)(g / (uint32_t)A.ny % (uint32_t)A.nx);
-        const int l = (int)(g / ((uint32_t)A.ny * (uint32_t)A.nx));
-        h += eyebox_add(A, l, m, n, p.x, p.y);
+    for (unsigned long long e = tid; e < nf * kQBlock; e += nth) {
+        {
+            const unsigned long long j = (unsigned long long)A.full_list[e / kQBlock] * kQBlock + e % kQBlock;
+            const uint32_t g = A.q_i[j];   // tile index (lambda * nx + m) * ny + n
+            const double2 p = A.q_xy[j];
+            const int n = (int)(g % (uint32_t)A.ny), m = (int)(g / (uint32_t)A.ny % (uint32_t)A.nx);
+            const int l = (int)(g / ((uint32_t)A.ny * (uint32_t)A.nx));
+            h += eyebox_add(A, l, m, n, p.x, p.y);
+        }
     }
     for (unsigned long long k = tid; k < nr; k += nth) {
         const int64_t i = (int64_t)A.replay_list[k];
@@ -126,6 +131,15 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
             A.rng[i] = st;
         }
     }
+    if (blockIdx.x == 0) {
+        for (int k = threadIdx.x; k < A.n_trace_waves; k += blockDim.x) {
+            const unsigned long long *slot = A.part + 4 * (size_t)k;
+            b += slot[0];
+            bad += slot[1];
+            h += slot[2];
+        }
+        if (threadIdx.x < kScratchCtr) A.other_ctr[threadIdx.x] = 0ull;
+    }
     const int w = threadIdx.x >> 6;
     b = wave_sum(b);
     bad = wave_sum(bad);
@@ -136,41 +150,6 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
         red[w][2] = h;
     }
     __syncthreads();
-    if (threadIdx.x == 0) {
-        unsigned long long *slot = A.part + 4 * ((size_t)A.n_trace_waves + blockIdx.x);
-        slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
-        slot[3] = 0;
-    }
-}
-
-// One workgroup after the epilogue: sums the partial slots of the trace kernel's and the
-// epilogue's workgroups into *stats (four atomics per launch) and zeroes the launch scratch
-// counters (queue heads, replay / queue counts) for the next launch on the stream, which
-// therefore needs no memset of its own.
-__global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilogue) {
-    __shared__ unsigned long long red[4][3];
-    const unsigned long long nr = *A.replay_count;
-    const int nslots = A.n_trace_waves + n_epilogue;
-    uint64_t s0 = 0, s1 = 0, s2 = 0;
-#pragma unroll 4
-    for (int k = threadIdx.x; k < nslots; k += blockDim.x) {
-        const unsigned long long *slot = A.part + 4 * (size_t)k;
-        s0 += slot[0];
-        s1 += slot[1];
-        s2 += slot[2];
-    }
-    s0 = wave_sum(s0);
-    s1 = wave_sum(s1);
-    s2 = wave_sum(s2);
-    const int w = threadIdx.x >> 6;
-    if ((threadIdx.x & 63) == 0) {
-        red[w][0] = s0;
-        red[w][1] = s1;
-        red[w][2] = s2;
-    }
-    __syncthreads();   // every thread has read the counts it needs before they are zeroed
     if (threadIdx.x == 0 && A.stats) {
         wgrt_trace_stats *st = A.stats;
         const unsigned long long t0 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
@@ -179,9 +158,8 @@ __global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilog
         if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
         if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
         if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
-        if (nr) atomicAdd((unsigned long long *)&st->replayed, nr);
+        if (blockIdx.x == 0 && nr) atomicAdd((unsigned long long *)&st->replayed, nr);
     }
-    if (threadIdx.x < kScratchCtrWords) A.heads0[threadIdx.x] = 0ull;
 }
 
 // Work queue of the Jones-vector variants: one head per XCD (each on its own 128-B line), head
@@ -191,9 +169,6 @@ __global__ __launch_bounds__(256) void finalize_kernel(TraceArgs A, int n_epilog
 // steers placement only: any wave may take any chunk, so correctness never depends on it.
 constexpr int kFusedRefill = 16;
 constexpr int64_t kStripe = 16;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
-constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
-                               // out-couples ~10 rays per trace; unused slots cost the eyebox
-                               // epilogue a read each)
 // Passes a fused-launch lane may wait for its ray's previous trace before it gives the ray up
 // (counted in wgrt_trace_stats.bad_rays).  A legitimate wait is bounded by that trace's length
 // (<= 1e5 + 1 bounces, at least one per pass of the wave running it); the bound only turns a
@@ -250,6 +225,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     uint32_t wait_passes = 0;          // fused: passes spent waiting for the current ray
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
+    bool qblk = false;                 // a block has been reserved
 
     // head x's items: iteration-major over its chunk range [lo, hi)
     // head x's items: stripes of kStripe consecutive chunks, stripe s on head s % 8, iteration-
@@ -445,14 +421,32 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 KA(q_i)[j] = L.tix;
             }
             if (nout > rem) {
+                // the old block is full: the epilogue bins it
+                if (qblk && lane == 0) KA(full_list)[atomicAdd(KA(full_count), 1ull)] = (uint32_t)(qbase / kQBlock);
                 qbase = nb;
                 qfill = nout - rem;
+                qblk = true;
             } else {
                 qfill += nout;
             }
         }
     }
-    for (int j = qfill + lane; j < kQBlock; j += 64) A.q_i[qbase + j] = 0xffffffffu;   // unused slots
+    // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one
+    // lane per entry, its own stores read back (agent-scope loads, past the L1)
+    uint32_t tot_h = 0;
+    if (qblk) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        if (lane < qfill) {
+            const uint32_t g = __hip_atomic_load(KA(q_i) + qbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double *pq = (const double *)(KA(q_xy) + qbase + lane);
+            const double px = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const double py = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const int ny = KA(ny), nx = KA(nx);
+            const int en = (int)(g % (uint32_t)ny), em = (int)(g / (uint32_t)ny % (uint32_t)nx);
+            const int el = (int)(g / ((uint32_t)ny * (uint32_t)nx));
+            tot_h = eyebox_add(A, el, em, en, px, py) ? 1u : 0u;
+        }
+    }
     if (tl_on && lane == 0) {
         tl[8 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
         tl[8 * tl_wave + 3] = tl_passes;
@@ -460,19 +454,21 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
     }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
-    __shared__ unsigned long long red[4][2];
+    __shared__ unsigned long long red[4][3];
     const uint64_t sum_b = wave_sum((uint64_t)tot_b);
     const uint64_t sum_bad = wave_sum((uint64_t)tot_bad);
+    const uint64_t sum_h = wave_sum((uint64_t)tot_h);
     if (lane == 0) {
         red[threadIdx.x >> 6][0] = sum_b;
         red[threadIdx.x >> 6][1] = sum_bad;
+        red[threadIdx.x >> 6][2] = sum_h;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
         unsigned long long *slot = KA(part) + 4 * (size_t)blockIdx.x;
         slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
         slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        slot[2] = 0;
+        slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
         slot[3] = 0;
     }
 }
@@ -853,6 +849,7 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
         (void)hipFree(kv.second.list);
         (void)hipFree(kv.second.q_xy);
         (void)hipFree(kv.second.q_i);
+        (void)hipFree(kv.second.full);
         (void)hipFree(kv.second.rng64);
         (void)hipFree(kv.second.part);
     }
@@ -884,19 +881,25 @@ namespace {
 // launch (epoch != NULL) the launch epoch of the granule tags is advanced here, under the same
 // lock, and returned.
 wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num_iter, int64_t grid,
-                           wgrt_scene::Scratch **out, uint32_t *epoch = nullptr) {
+                           wgrt_scene::Scratch **out, uint32_t *epoch = nullptr, uint32_t *parity = nullptr) {
     hipStream_t st = (hipStream_t)stream;
     std::lock_guard<std::mutex> lk(ms->scratch_mu);
     wgrt_scene::Scratch *sc = &ms->scratch[stream];
     *out = sc;
     if (!sc->ctr) {
-        // zeroed once here; afterwards every launch's epilogue leaves the counters zeroed
-        hipError_t e = hipMalloc((void **)&sc->ctr, kScratchCtr * sizeof(unsigned long long));
-        if (e == hipSuccess) e = hipMemset(sc->ctr, 0, kScratchCtr * sizeof(unsigned long long));
+        // both counter sets zeroed once here; afterwards every launch's epilogue zeroes the set
+        // the next launch uses
+        hipError_t e = hipMalloc((void **)&sc->ctr, 2 * kScratchCtr * sizeof(unsigned long long));
+        if (e == hipSuccess) e = hipMemset(sc->ctr, 0, 2 * kScratchCtr * sizeof(unsigned long long));
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+        sc->parity = 0;
     }
-    // counter partials: one slot per trace-kernel workgroup and per epilogue workgroup
-    const int64_t slots = grid + kEpilogueGroups;
+    if (parity) {   // a launch: its counter set, and the next launch takes the other one
+        *parity = sc->parity;
+        sc->parity ^= 1u;
+    }
+    // counter partials: one slot per trace-kernel workgroup
+    const int64_t slots = grid;
     if (sc->part_slots < slots) {
         HIP_TRY(hipStreamSynchronize(st));
         (void)hipFree(sc->part);
@@ -923,11 +926,14 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
         HIP_TRY(hipStreamSynchronize(st));
         (void)hipFree(sc->q_xy);
         (void)hipFree(sc->q_i);
+        (void)hipFree(sc->full);
         sc->q_xy = nullptr;
         sc->q_i = nullptr;
+        sc->full = nullptr;
         sc->qcap = 0;
         hipError_t e = hipMalloc((void **)&sc->q_xy, (size_t)qn * sizeof(double2));
         if (e == hipSuccess) e = hipMalloc((void **)&sc->q_i, (size_t)qn * sizeof(uint32_t));
+        if (e == hipSuccess) e = hipMalloc((void **)&sc->full, (size_t)(qn / kQBlock + 1) * sizeof(uint32_t));
         if (e == hipErrorOutOfMemory) return fail(WGRT_ERR_OUT_OF_MEMORY, "hipMalloc(launch scratch): out of memory");
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
         sc->qcap = qn;
@@ -1038,22 +1044,27 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     if (grid > useful) grid = useful;
     wgrt_scene *ms = const_cast<wgrt_scene *>(s);
     wgrt_scene::Scratch *sc = nullptr;
-    uint32_t epoch = 0;
+    uint32_t epoch = 0, parity = 0;
     {
-        const wgrt_status e = ensure_scratch(ms, stream, n_rays, num_iter, grid, &sc, num_iter > 1 ? &epoch : nullptr);
+        const wgrt_status e =
+            ensure_scratch(ms, stream, n_rays, num_iter, grid, &sc, num_iter > 1 ? &epoch : nullptr, &parity);
         if (e != WGRT_OK) return e;
     }
+    unsigned long long *const ctr = sc->ctr + (size_t)parity * kScratchCtr;
     if (num_iter > 1) {
         A.n_iter = num_iter;
         A.rng64 = sc->rng64;
         A.iter_epoch = epoch;
     }
-    A.replay_count = sc->ctr + kHeads * kHeadStride;
+    A.replay_count = ctr + kHeads * kHeadStride;
     A.replay_list = sc->list;
     A.q_xy = sc->q_xy;
     A.q_i = sc->q_i;
-    A.q_count = sc->ctr + (kHeads + 1) * kHeadStride;
-    A.heads0 = sc->ctr;
+    A.q_count = ctr + (kHeads + 1) * kHeadStride;
+    A.full_count = ctr + (kHeads + 2) * kHeadStride;
+    A.full_list = sc->full;
+    A.heads0 = ctr;
+    A.other_ctr = sc->ctr + (size_t)(parity ^ 1u) * kScratchCtr;
     A.part = sc->part;
     A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
     const int jchunk = A.order ? kChunk : g_jchunk;   // chunk_order is given in 64-ray chunks
@@ -1062,13 +1073,13 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
 #define WGRT_LAUNCH_JONES(CELL, LOCV)                                                                              \
     do {                                                                                                           \
         if (num_iter > 1 && single)                                                                                \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, true>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk);  \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, true>), g3, b3, 0, st, A, LOCV, ctr, jchunk);  \
         else if (num_iter > 1)                                                                                     \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, false>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk); \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, false>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
         else if (single)                                                                                           \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, true>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk); \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, true>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
         else                                                                                                       \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false>), g3, b3, 0, st, A, LOCV, sc->ctr, jchunk);\
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false>), g3, b3, 0, st, A, LOCV, ctr, jchunk);\
     } while (0)
     if (variant == 9) {
         WGRT_LAUNCH_JONES(uint64_t, A.loc);
@@ -1079,8 +1090,6 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
 #undef WGRT_LAUNCH_JONES
     HIP_TRY(hipGetLastError());
     hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(finalize_kernel, dim3(1), dim3(256), 0, st, A, kEpilogueGroups);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }
