@@ -101,7 +101,10 @@ constexpr int kScratchCtr = (kHeads + 3) * kHeadStride;   // heads, replay / que
 //  4. zeroes the other counter set, which the next launch on the stream uses (this launch's set
 //     is still being read by the other workgroups; the launch after next finds it zeroed).
 constexpr int kEpilogueGroups = 256;
-constexpr int kQBlock = 32;    // out-coupling queue slots a wave reserves at a time (a C3 wave
+#ifndef WGRT_QBLOCK
+#define WGRT_QBLOCK 32
+#endif
+constexpr int kQBlock = WGRT_QBLOCK;    // out-coupling queue slots a wave reserves at a time (a C3 wave
                                // out-couples ~10 rays per trace)
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
@@ -168,7 +171,10 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
 // spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The XCD id
 // steers placement only: any wave may take any chunk, so correctness never depends on it.
 constexpr int kFusedRefill = 16;
-constexpr int64_t kStripe = 16;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
+#ifndef WGRT_STRIPE
+#define WGRT_STRIPE 16
+#endif
+constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
 // Passes a fused-launch lane may wait for its ray's previous trace before it gives the ray up
 // (counted in wgrt_trace_stats.bad_rays).  A legitimate wait is bounded by that trace's length
 // (<= 1e5 + 1 bounces, at least one per pass of the wave running it); the bound only turns a
