@@ -8,10 +8,10 @@ Same flow as the reference script, on the MI355X kernel:
 3. ray batch: ``num_rays_per_FoV / 2`` in-coupler origins shared by every FoV x wavelength
    block, TE then TM halves (MAIN:59-115), RNG seeds ``0x9E3779B9 * (gid + 1)`` (MAIN:158),
    laid out on the device by ``wgrt_rays_init``;
-4. ``num_iter`` chained launches of the bounce kernel (MAIN:169-177), by default as one fused
-   call (``num_iter`` traces per ray in one persistent launch; identical results; ``fuse=False``
-   issues separate launches), timed with HIP events (no JIT in the timed region, unlike the
-   reference's wall clock);
+4. ``num_iter`` chained launches of the bounce kernel (MAIN:169-177), as one fused call
+   (``num_iter`` traces per ray in one persistent launch; identical results) when a GPU traces
+   at most ``FUSE_MAX_RAYS`` rays, else as separate launches (``fuse`` overrides), timed with HIP
+   events (no JIT in the timed region, unlike the reference's wall clock);
 5. efficiencies ``A = sum(EB) / N / num_iter``, ``eff_c = 3 * sum(A[lambda])`` (MAIN:186-192)
    and ``evaluation(EB / R / num_iter)`` (MAIN:197-198).
 
@@ -29,10 +29,17 @@ import time
 import numpy as np
 
 
+# Fusing the num_iter chained traces into one persistent launch overlaps each trace's tail with
+# the next one's bulk: 1.5x faster at 1.35M rays per GPU (C3), even at 5.4M (C4), and 13 % slower
+# at 82.6M (C5, where the tail is a small part of a launch and the fused kernel runs one wave per
+# SIMD fewer).  fuse=None picks by the rays per GPU.
+FUSE_MAX_RAYS = 4_000_000
+
+
 def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000, num_iter: int = 4,
         lambdas=(0, 1, 2), lut_dir: str | None = None, lut_seed: int = 0, lut_profile: str = "default",
         point_seed: int | None = None, evaluate: bool = True, verbose: bool = True, variant: int = 0,
-        fuse: bool = True) -> dict:
+        fuse: bool | None = None) -> dict:
     import torch
     import torch.distributed as dist
 
@@ -73,6 +80,8 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
 
     # the num_iter chained launches of MAIN:169-177; fuse: as one call (wgrt_launch_opts.num_iter,
     # one persistent launch for the Jones-vector variants), with results identical to num_iter calls
+    if fuse is None:
+        fuse = shard.n_rays <= FUSE_MAX_RAYS
     per_call = 0 if fuse else 1
     calls = split_calls(num_iter, per_call)
     if shard.n_rays and calls:
@@ -125,7 +134,9 @@ def main(argv=None):
     ap.add_argument("--lut-profile", default="default")
     ap.add_argument("--point-seed", type=int, default=None)
     ap.add_argument("--no-eval", action="store_true")
-    ap.add_argument("--no-fuse", action="store_true", help="issue num_iter separate launches")
+    ap.add_argument("--fuse", choices=["auto", "yes", "no"], default="auto",
+                    help="num_iter chained traces as one fused launch (auto: when a GPU traces <= 4M rays)")
+    ap.add_argument("--no-fuse", action="store_true", help="same as --fuse no")
     ap.add_argument("--json", default=None, help="write scalar results here")
     a = ap.parse_args(argv)
     import torch
@@ -135,7 +146,8 @@ def main(argv=None):
         torch.cuda.set_device(local)
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     res = run(a.num_fov_x, a.num_fov_y, a.rays_per_fov, a.num_iter, lut_dir=a.lut_dir, lut_seed=a.lut_seed,
-              lut_profile=a.lut_profile, point_seed=a.point_seed, evaluate=not a.no_eval, fuse=not a.no_fuse)
+              lut_profile=a.lut_profile, point_seed=a.point_seed, evaluate=not a.no_eval,
+              fuse=False if a.no_fuse else {"auto": None, "yes": True, "no": False}[a.fuse])
     if a.json and (not dist.is_initialized() or dist.get_rank() == 0):
         keep = {k: v for k, v in res.items() if isinstance(v, (int, float, dict, str))}
         with open(a.json, "w") as f:
