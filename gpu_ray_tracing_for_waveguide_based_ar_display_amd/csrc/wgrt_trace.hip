@@ -53,11 +53,14 @@ double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
     return v ? atof(v) : 0.0078125;   // 1/128 mm: 71 MB grid at C3; fewer EDGE-cell exact tests (fastest on C3)
 }();
-// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK, multiple of 64)
+// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK)
+#ifndef WGRT_JCHUNK_DEFAULT
+#define WGRT_JCHUNK_DEFAULT 64
+#endif
 int g_jchunk = [] {
     const char *v = getenv("WGRT_JCHUNK");
-    const int c = v ? atoi(v) : 64;
-    return c >= 64 ? c / 64 * 64 : 64;
+    const int c = v ? atoi(v) : WGRT_JCHUNK_DEFAULT;
+    return c >= 1 ? c : WGRT_JCHUNK_DEFAULT;
 }();
 double g_cert_tol = 1e-10;   // Jones-vector variants' double-precision certification bound (wgrt_debug_set_cert_tol)
 // ... and the single-precision estimate's (wgrt_debug_set_cert_tol32): 8e-6 covers the rounding of
@@ -208,8 +211,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
     int head = xcc_id();
-    int pend_h = -1;                  // head of the dequeue in flight (-1: none)
-    unsigned long long pend_v = 0;    // its result (lane 0)
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
     // debug timeline (wgrt_debug_set_timeline; NULL in production): per wave, start / queue
     // exhausted / end (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD,
@@ -221,7 +222,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     if (tl_on && lane == 0) tl[8 * tl_wave] = __builtin_amdgcn_s_memrealtime();
     uint32_t cur_k = 0;               // the item's iteration
     bool exhausted = false;
-    bool active = false, waiting = false;
+    bool active = false, waiting = false, taken = false;
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
@@ -233,7 +234,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
     bool qblk = false;                 // a block has been reserved
 
-    // head x's items: iteration-major over its chunk range [lo, hi)
     // head x's items: stripes of kStripe consecutive chunks, stripe s on head s % 8, iteration-
     // major.  Every die gets a mix of all FoVs and wavelengths -- ray lifetimes differ by tile,
     // and with one contiguous eighth of the tiles per head the die holding the long-lived tiles
@@ -331,16 +331,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         if (FUSED && __popcll(need) < kFusedRefill && __ballot(active || waiting) != 0ull) need = 0ull;
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
-                // the dequeue for this item was issued when the previous one started (pend_v,
-                // on head pend_h): its latency overlapped that item's passes
+                // dequeue an item when it is needed.  Claiming the next item ahead (to hide the
+                // atomic's latency) doubled the rays a wave holds when the queue runs dry, and the
+                // launch's tail with them: single launches ran 3 % slower with it
                 int64_t c = -1;
                 uint32_t k = 0;
                 bool got = false;
-                if (pend_h >= 0) {
-                    const unsigned long long pq = __shfl(pend_v, 0);
-                    got = decode(pend_h, (int64_t)pq, c, k);
-                    if (!got) head = (pend_h + 1) & (kHeads - 1);   // that head ran dry: move on
-                }
                 for (int tries = 0; !got && tries < kHeads; ++tries) {
                     const int x = (head + tries) & (kHeads - 1);
                     unsigned long long q = 0;
@@ -351,7 +347,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                         got = true;
                     }
                 }
-                pend_h = -1;
                 if (!got) {
                     exhausted = true;
                     if (tl_on && lane == 0) {
@@ -361,8 +356,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                     }
                     break;
                 }
-                pend_h = head;   // issue the next dequeue now; read when this item runs dry
-                if (lane == 0) pend_v = atomicAdd(heads + kHeadStride * head, 1ull);
                 const int32_t *const ord = KA(order);
                 const int64_t cc = (!FUSED && ord) ? (int64_t)ord[c] : c;
                 cur = cc * chunk;
@@ -373,16 +366,22 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             const int want = __popcll(need);
             const int64_t avail = end - cur;
             const int take = (int64_t)want < avail ? want : (int)avail;
-            if (!active && !waiting) {
+            if ((need >> lane) & 1ull) {
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
                 if (rank < take) {
                     L.i = cur + rank;
                     L.k = cur_k;
-                    start();
+                    taken = true;
                 }
             }
             cur += take;
-            need = __ballot(!active && !waiting);
+            need = __ballot(!active && !waiting && !taken);
+        }
+        // the rays taken from every item of this refill start together: one round trip for
+        // their columns however many items they came from
+        if (taken) {
+            start();
+            taken = false;
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
         if (tl_on) {
@@ -481,7 +480,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
 // Variants 7 / 9: the persistent loop over the Jones-vector path (32-bit cell words; 64-bit
 // cell words for scenes of more than 16 polygons).  Waves per SIMD: 5 for the full-colour
-// single-trace kernel over 32-bit cells (<= 96 VGPRs, no spills; 2 % faster than 4 on C3), 4 for
+// single-trace kernel over 32-bit cells (96 VGPRs + 12 B/lane of scratch; 2 % faster than 4 on C3), 4 for
 // the others (<= 128 VGPRs: at 96 they spill).
 #ifndef WGRT_JONES_WAVES
 #define WGRT_JONES_WAVES 5

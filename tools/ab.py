@@ -34,13 +34,26 @@ eb = torch.zeros(sc.eb_shape(), dtype=torch.float32, device=dev)
 st = torch.zeros(4, dtype=torch.int64, device=dev)
 nl, nf = int(os.environ["AB_LAUNCHES"]), int(os.environ["AB_FUSED"])
 reserve(sc, rays["x"].numel(), nf)
-for _ in range(3): trace_fullcolor(sc, rays, rng, eb)
+order = None
+if os.environ.get("AB_ORDER"):   # lifetime-ordered chunk issue from one earlier launch
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import schedule_by_lifetime, CHUNK
+    pb = torch.zeros(rays["x"].numel(), dtype=torch.int32, device=dev)
+    trace_fullcolor(sc, rays, rng.clone(), eb.clone(), per_ray_bounces=pb)
+    key = ((rays["lmd_num"].to(torch.int64) * nx + rays["m"].to(torch.int64)) * ny + rays["n"].to(torch.int64))
+    if os.environ["AB_ORDER"] == "seg":
+        order = schedule_by_lifetime(pb, key, nx * ny * 3)
+    else:
+        tot = torch.zeros(nx * ny * 3, device=dev).index_add_(0, key, pb.float())
+        cnt = torch.zeros(nx * ny * 3, device=dev).index_add_(0, key, torch.ones_like(pb, dtype=torch.float32))
+        ck = (tot / cnt.clamp_min(1))[key[::CHUNK]]
+        order = torch.argsort(-ck, stable=True).to(torch.int32)
+for _ in range(3): trace_fullcolor(sc, rays, rng, eb, chunk_order=order)
 trace_fullcolor(sc, rays, rng, eb, num_iter=2)
 torch.cuda.synchronize()
 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl + 1)]
 st.zero_()
 for k in range(nl):
-    ev[k][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st); ev[k][1].record()
+    ev[k][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st, chunk_order=order); ev[k][1].record()
 torch.cuda.synchronize()
 b1 = int(st[0]) / nl
 st.zero_()
@@ -63,9 +76,11 @@ def main():
     res = {n: [] for n in a.names}
     for r in range(a.rounds):
         for n in a.names:
-            lib = os.path.join(REPO, "exp_libs", n, "libwgrt.so") if n != "tree" else ""
+            # NAME[:seg|:glob]: the build, optionally with lifetime-ordered chunk issue
+            build, _, order = n.partition(":")
+            lib = os.path.join(REPO, "exp_libs", build, "libwgrt.so") if build != "tree" else ""
             env = dict(os.environ, REPO=REPO, AB_CONFIG=a.config, AB_LAUNCHES=str(a.launches),
-                       AB_FUSED=str(a.fused), WGRT_LIB=lib)
+                       AB_FUSED=str(a.fused), WGRT_LIB=lib, AB_ORDER=order)
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(p.stderr[-3000:])
