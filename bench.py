@@ -62,6 +62,11 @@ def parse(argv=None):
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
     ap.add_argument("--no-extras", action="store_true", help="skip the main_job / fused rates")
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
+                    help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
+                         "N > 1 path on a one-GPU box together with --one-device)")
+    ap.add_argument("--one-device", action="store_true",
+                    help="rehearsal: every rank uses cuda:0 (with --dist-backend gloo)")
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC traffic per bounce (tools/pmc_traffic.py), used when its library hash matches")
@@ -103,10 +108,17 @@ def main(argv=None):
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.one_device:
+        if a.dist_backend != "gloo":
+            raise SystemExit("--one-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
+        local = 0
     torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
     if world > 1:
-        dist.init_process_group("nccl", device_id=dev)
+        if a.dist_backend == "nccl":
+            dist.init_process_group("nccl", device_id=dev)
+        else:
+            dist.init_process_group("gloo")
 
     cname, cfg = config_for(a.config, world)
     nx, ny, lambdas, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
@@ -183,7 +195,10 @@ def main(argv=None):
             "config": {"workload": f"{cname}: {cfg['name']}", "nx": nx, "ny": ny, "lambdas": lambdas,
                        "num_rays_per_FoV": R, "rays_total": nx * ny * len(lambdas) * R, "rays_rank0": shard.n_rays,
                        "lut": f"synthetic seed {a.lut_seed} profile {cfg['profile']}",
-                       "parallelism": f"fov-lambda block shards x{world}" + (" + RCCL reduce(EB)" if world > 1 else ""),
+                       "parallelism": f"fov-lambda block shards x{world}" + (
+                           (" + RCCL reduce(EB)" if a.dist_backend == "nccl" else
+                            " + gloo reduce(EB), rehearsal" + (" on one GPU" if a.one_device else ""))
+                           if world > 1 else ""),
                        "kernel_variant": a.variant, "steps_per_launch": 1, "lib_sha16": sha,
                        "scene_create_s": round(t_scene, 3)},
             "roofline": roofline,

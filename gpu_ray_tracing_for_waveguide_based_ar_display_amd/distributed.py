@@ -84,7 +84,11 @@ def reduce_eyebox(eb, group=None, dst: int = 0):
     """Sum-reduce the eyebox grid to ``dst`` (exact: integer counts in float32 < 2**24)."""
     import torch.distributed as dist
     if dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.reduce(eb, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if getattr(eb, "is_cuda", False) and dist.get_backend(group) == "gloo":
+            # gloo reduces device tensors only as an all-reduce (the bench's one-GPU rehearsal)
+            dist.all_reduce(eb, op=dist.ReduceOp.SUM, group=group)
+        else:
+            dist.reduce(eb, dst=dst, op=dist.ReduceOp.SUM, group=group)
     return eb
 
 
