@@ -25,6 +25,7 @@ def main():
     ap.add_argument("--variant", type=int, default=0)
     ap.add_argument("--reps", type=int, default=3)
     ap.add_argument("--out", default=None)
+    ap.add_argument("--raw", default=None, help="also save the per-wave records (npz)")
     ap.add_argument("--order", default="none", choices=["none", "lifetime"],
                     help="chunk issue order: ascending, or long-lived tiles first (from a previous launch)")
     a = ap.parse_args()
@@ -84,10 +85,17 @@ def main():
              "drain_passes": [float(np.percentile(passes - p_exh, q)) for q in (0, 50, 100)],
              "drain_lanes_per_pass": float((lanes - l_exh).sum() / max((passes - p_exh).sum(), 1)),
              "bulk_lanes_per_pass": float(l_exh.sum() / max(p_exh.sum(), 1)),
+             # the waves that end the launch: their drain passes' mean duration (the critical chain)
+             "last1pct_drain_us_per_pass": float(np.median(((end - exh) / 100.0 / np.maximum(passes - p_exh, 1))[
+                 us(end) >= np.percentile(us(end), 99)])),
+             "last1pct_drain_passes": float(np.median((passes - p_exh)[us(end) >= np.percentile(us(end), 99)])),
              "waves_alive_at_us": {int(tt): int(((us(start) <= tt) & (us(end) > tt)).sum())
                                    for tt in (100, 200, 250, 300, 350, 400)},
              "end_by_xcd_us": {int(x): float(us(end[xcc == x]).max()) for x in np.unique(xcc)},
              "exhausted_by_xcd_us": {int(x): float(us(exh[xcc == x]).max()) for x in np.unique(xcc)}}
+        if a.raw:
+            np.savez_compressed(f"{a.raw}.{rep}.npz", start=start, exh=exh, end=end, passes=passes, lanes=lanes,
+                                xcc=xcc, p_exh=p_exh, l_exh=l_exh)
         r["order"] = a.order
         r["drain_hops"] = int(os.environ.get("WGRT_DRAIN_HOPS", "1"))
         res.append(r)
