@@ -64,11 +64,18 @@ constexpr int kJHop = 8;          // (cos, sin) of 2 lut_TIR[0] (R2 miss hop), o
 constexpr int kJCosIc1 = 12;      // cos(lut_ic1[l, m, n, 0].real)
 constexpr int kJGrowth = 13;      // max(1, max_k |lut_TIR[k]| / pi): bounds the reference's unwrapped phase growth
 constexpr int kJHeader = 16;
-constexpr int kJBlock = 48;       // cosA[3], Wsum, rec32[3][8] (floats), rec[3][8], W[3], pad
-constexpr int kJBlockCos = 0;
-constexpr int kJBlockWsum = 3;    // sum of W[k]
-constexpr int kJBlockRec32 = 4;   // the three matrices rounded to float (96 B): the estimate's input
+// Block line 0 (the estimate's input, read by every interaction): cosA_0, cosA_1 (double), then
+// four floats {Wsum, cosA_2, 0, 0}, then per branch the Hermitian form H = M^H M of its matrix
+// M = [[p, r], [q, s]] as four floats {h11, h22, Re h12, Im h12}: |M E|^2 = h11 |Ete|^2 +
+// h22 |Etm|^2 + 2 Re(h12 conj(Ete) Etm) -- half the bytes and a quarter of the products of
+// evaluating M E.  Lines 1-2: the matrices in double precision (the taken branch's field, the
+// rare double-precision re-evaluation), the bounds W[k] and cosA_2 in double.
+constexpr int kJBlock = 48;       // line 0: cosA[2], f32 {Wsum, cosA_2}, herm32[3][4]; rec[3][8], W[3], cosA_2
+constexpr int kJBlockCos = 0;     // cosA_0, cosA_1
+constexpr int kJBlockF32 = 2;     // floats: Wsum (sum of W[k], rounded up), cosA_2, 0, 0
+constexpr int kJBlockHerm = 4;    // floats [3][4]: h11, h22, Re h12, Im h12
 constexpr int kJBlockRec = 16;    // the three matrices in double precision
+constexpr int kJBlockCos2 = 43;   // cosA_2 in double
 // W[k] = ((|p|+|r|)^2 + (|q|+|s|)^2) * |cosA_k| * f_k (f_k the n_g factor of the branch): for a
 // field state E, |M_k E|^2 * cosA_k * f_k is computed to within D * W[k] * |E|^2 by any two
 // evaluations whose states and matrices agree to within D / 4 (relative) -- the bound the

@@ -594,14 +594,8 @@ enum : int { kUncertain = -3, kOut = -4 };
 // Every column load is issued before anything branches on a loaded value, so a refill waits
 // for one memory round trip (not one for the FoV / wavelength indices and another for the
 // rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
-__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
-                                          uint64_t *gword = nullptr) {
-    const int64_t ld = i;
-    const float *const cl = KA(l);
-    const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
-    const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
-    const uint32_t rs = KA(rng)[ld];
-    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+__device__ __forceinline__ bool lane_init(const TraceArgs &A, int64_t i, JLane &L, float fx, float fy, float fm,
+                                          float fn, float fl, float fte, float ftm, float d, uint32_t rs) {
     const int m = (int)fm, n = (int)fn, l = (int)fl;
     const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
     L.i = (uint32_t)i;
@@ -626,6 +620,57 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &
     L.bounces = 1;
     L.pf = 0ull;
     return ok;
+}
+
+__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
+                                          uint64_t *gword = nullptr) {
+    const int64_t ld = i;
+    const float *const cl = KA(l);
+    const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
+    const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
+    const uint32_t rs = KA(rng)[ld];
+    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return lane_init(A, i, L, fx, fy, fm, fn, fl, fte, ftm, d, rs);
+}
+
+// Ray columns staged in LDS a work-queue chunk at a time: the wave that dequeues a chunk of
+// at most 64 rays copies their nine columns (wgrt_rays order below; lmd_num 0 when absent)
+// into its LDS buffer with one direct-to-LDS load per column (lane j <- ray base + j: no
+// VGPR destinations, every lane of the wave busy), and the lanes it refills from that chunk
+// later read their ray from there.  A refill then costs LDS reads instead of nine per-lane
+// gathers and a memory round trip, except right after a dequeue.
+constexpr int kStageCols = 9;   // x, y, m, n, lmd_num, te, tm, delta_phase, rng
+typedef uint32_t __attribute__((address_space(3))) LdsU32;
+
+__device__ __forceinline__ void glds4(const void *g, LdsU32 *dst) {
+    __builtin_amdgcn_global_load_lds(g, (void __attribute__((address_space(3))) *)dst, 4, 0, 0);
+}
+
+// Issued by the lanes j < n of a wave (exec-masked): column c of ray base + j -> S[c * 64 + j].
+__device__ __forceinline__ void stage_chunk(const TraceArgs &A, LdsU32 *S, int64_t ray) {
+    glds4(KA(x) + ray, S + 0 * 64);
+    glds4(KA(y) + ray, S + 1 * 64);
+    glds4(KA(m) + ray, S + 2 * 64);
+    glds4(KA(n) + ray, S + 3 * 64);
+    const float *const cl = KA(l);
+    if (cl) glds4(cl + ray, S + 4 * 64);
+    glds4(KA(te) + ray, S + 5 * 64);
+    glds4(KA(tm) + ray, S + 6 * 64);
+    glds4(KA(dph) + ray, S + 7 * 64);
+    glds4(KA(rng) + ray, S + 8 * 64);
+}
+
+// lane_load from a staged chunk: slot j of buffer S (the loads that filled it have landed).
+__device__ __forceinline__ bool lane_load_staged(const TraceArgs &A, const LdsU32 *S, int j, int64_t i, JLane &L,
+                                                 const uint64_t *granule = nullptr, uint64_t *gword = nullptr) {
+    const float fx = __uint_as_float(S[0 * 64 + j]), fy = __uint_as_float(S[1 * 64 + j]);
+    const float fm = __uint_as_float(S[2 * 64 + j]), fn = __uint_as_float(S[3 * 64 + j]);
+    const float fl = KA(l) ? __uint_as_float(S[4 * 64 + j]) : 0.0f;
+    const float fte = __uint_as_float(S[5 * 64 + j]), ftm = __uint_as_float(S[6 * 64 + j]);
+    const float d = __uint_as_float(S[7 * 64 + j]);
+    const uint32_t rs = S[8 * 64 + j];
+    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    return lane_init(A, i, L, fx, fy, fm, fn, fl, fte, ftm, d, rs);
 }
 
 struct JField {
@@ -681,23 +726,11 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
     return L.cells[iy * L.ncx + ix];
 }
 
-// One interaction block's single-precision copy of its Jones matrices (p, q, r, s per branch).
-struct Rec32 {
-    float pr, pi, qr, qi, rr, ri, sr, si;
-};
-
-__device__ __forceinline__ Rec32 load_rec32(const float *p) {
-    const float4 a = *(const float4 *)p, b = *(const float4 *)(p + 4);
-    return Rec32{a.x, a.y, a.z, a.w, b.x, b.y, b.z, b.w};
-}
-
-// |M E|^2 in single precision (the certified estimate of a branch efficiency's numerator).
-__device__ __forceinline__ float norm2_32(const Rec32 &c, float er, float ei, float mr, float mi) {
-    const float yr = fmaf(c.pr, er, fmaf(-c.pi, ei, fmaf(c.rr, mr, -c.ri * mi)));
-    const float yi = fmaf(c.pr, ei, fmaf(c.pi, er, fmaf(c.rr, mi, c.ri * mr)));
-    const float zr = fmaf(c.qr, er, fmaf(-c.qi, ei, fmaf(c.sr, mr, -c.si * mi)));
-    const float zi = fmaf(c.qr, ei, fmaf(c.qi, er, fmaf(c.sr, mi, c.si * mr)));
-    return fmaf(yr, yr, fmaf(yi, yi, fmaf(zr, zr, zi * zi)));
+// |M E|^2 in single precision from the block's Hermitian form H = M^H M (the certified estimate
+// of a branch efficiency's numerator): h11 |Ete|^2 + h22 |Etm|^2 + 2 Re(h12 conj(Ete) Etm),
+// with a = |Ete|^2, b = |Etm|^2, (cr, ci) = conj(Ete) Etm shared by every branch.
+__device__ __forceinline__ float herm_form(const float4 &h, float a, float b, float cr, float ci) {
+    return fmaf(h.x, a, fmaf(h.y, b, 2.0f * fmaf(h.z, cr, -h.w * ci)));
 }
 
 // A Monte-Carlo decision of the Jones-vector lane: the branch efficiencies a_k (estimates of the
@@ -740,15 +773,27 @@ __device__ __forceinline__ void jones_decide(JDecision &d, double u, double scl,
     d.ok = ok;
 }
 
-// The efficiencies from the single-precision matrices (the estimate every decision starts with).
+// A block's {cosA_0, cosA_1, cosA_2, Wsum} for the estimate: cosA_0 and cosA_1 in double (the
+// taken branch's efficiency uses them), cosA_2 and Wsum from their floats (the exact cosA_2 is
+// read only by the rare double-precision re-evaluation, estimate64).
+__device__ __forceinline__ double4 block_cw(const double *B) {
+    const double2 c01 = *(const double2 *)(B + kJBlockCos);
+    const float4 fw = *(const float4 *)(B + kJBlockF32);
+    return double4{c01.x, c01.y, (double)fw.y, (double)fw.x};
+}
+
+// The efficiencies from the single-precision Hermitian forms (the estimate every decision starts
+// with).  cw = {cosA_0, cosA_1, cosA_2, Wsum}.
 __device__ __forceinline__ void estimate32(JDecision &d, const double *B, const JRay &r, bool three, double inv,
                                            double f01, double inv_n_g, const double4 &cw) {
-    const float *R = (const float *)(B + kJBlockRec32);
-    const Rec32 k0 = load_rec32(R), k1 = load_rec32(R + 8);
+    const float4 *H = (const float4 *)(B + kJBlockHerm);
+    const float4 h0 = H[0], h1 = H[1];
     const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
-    const double q0 = (double)norm2_32(k0, er, ei, mr, mi), q1 = (double)norm2_32(k1, er, ei, mr, mi);
+    const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
+    const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
+    const double q0 = (double)herm_form(h0, a, b, cr, ci), q1 = (double)herm_form(h1, a, b, cr, ci);
     double q2 = 0.0;
-    if (three) q2 = (double)norm2_32(load_rec32(R + 16), er, ei, mr, mi);
+    if (three) q2 = (double)herm_form(H[2], a, b, cr, ci);
     d.a0 = q0 * cw.x * inv * f01;
     d.a1 = q1 * cw.y * inv * f01;
     d.a2 = three ? q2 * cw.z * inv * inv_n_g : 0.0;
@@ -768,7 +813,7 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
     }
     d.a0 = q[0] * cw.x * inv * f01;
     d.a1 = q[1] * cw.y * inv * f01;
-    d.a2 = three ? q[2] * cw.z * inv * inv_n_g : 0.0;
+    d.a2 = three ? q[2] * B[kJBlockCos2] * inv * inv_n_g : 0.0;
 }
 
 // Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
@@ -796,7 +841,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
     const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
-    const double4 cw = *(const double4 *)(B + kJBlockCos);        // cosA_0..2, Wsum
+    const double4 cw = block_cw(B);
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     if (r.hops) {
         const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));

@@ -174,8 +174,11 @@ WGRT_HD void pack_tile(const PackView &v, int64_t g, double *T, double *J) {
         // states) TIR[0] / TIR[2], FC blocks TIR[0] / TIR[1], OC blocks TIR[1] / TIR[3]
         const int ta = b < 3 ? 0 : (three ? 1 : 0), tb = b < 3 ? 2 : (three ? 3 : 1);
         double sum = 0.0;
+        O[kJBlockCos] = Bt[kBlockCos];
+        O[kJBlockCos + 1] = Bt[kBlockCos + 1];
+        O[kJBlockCos2] = Bt[kBlockCos + 2];
+        float *const f32 = (float *)(O + kJBlockF32);
         for (int k = 0; k < 3; ++k) {
-            O[kJBlockCos + k] = Bt[kBlockCos + k];
             double *rec = O + kJBlockRec + 8 * k;
             for (int j = 0; j < 8; ++j) rec[j] = Bt[kBlockRec + 8 * k + j];
             double w = 0.0;
@@ -197,10 +200,20 @@ WGRT_HD void pack_tile(const PackView &v, int64_t g, double *T, double *J) {
             }
             O[kJBlockW + k] = w;
             sum += w;
-            float *r32 = (float *)(O + kJBlockRec32) + 8 * k;   // the estimate's single-precision copy
-            for (int j = 0; j < 8; ++j) r32[j] = (float)rec[j];
+            // the estimate's single-precision Hermitian form H = M^H M (M = [[p, r], [q, s]]; the TIR
+            // turn of the TM row does not change it)
+            const double pr = rec[0], pi = rec[1], qr = rec[2], qi = rec[3];
+            const double rr = rec[4], ri = rec[5], sr = rec[6], si = rec[7];
+            float *h = (float *)(O + kJBlockHerm) + 4 * k;
+            h[0] = (float)((pr * pr + pi * pi) + (qr * qr + qi * qi));
+            h[1] = (float)((rr * rr + ri * ri) + (sr * sr + si * si));
+            h[2] = (float)((pr * rr + pi * ri) + (qr * sr + qi * si));   // Re(conj(p) r + conj(q) s)
+            h[3] = (float)((pr * ri - pi * rr) + (qr * si - qi * sr));   // Im(conj(p) r + conj(q) s)
         }
-        O[kJBlockWsum] = sum * 1.01;
+        f32[0] = (float)(sum * 1.01);   // 1.01: covers this bound's own rounding to float
+        f32[1] = (float)Bt[kBlockCos + 2];
+        f32[2] = 0.0f;
+        f32[3] = 0.0f;
     }
 }
 

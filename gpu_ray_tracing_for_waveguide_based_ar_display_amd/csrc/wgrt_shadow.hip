@@ -150,7 +150,7 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
                 jr.mi = fma(mr, hp.y, jr.mi * hp.x);
             }
             hops = 0;
-            const double4 cw = *(const double4 *)(JB + kJBlockCos);
+            const double4 cw = block_cw(JB);
             const double jden = entry ? J[kJCosIc1] : cos_th;
             const double inv = rcp_nr(jden);
             const double f01 = entry ? A.n_g : 1.0;

@@ -1,8 +1,9 @@
 """The device scene build (wgrt_scene_create: locator cell words by edge_mark_kernel /
 classify_cells_kernel, LUT tiles by pack_tiles_kernel) against the host build of the same rules
 (wgrt_debug_set_host_scene): identical cell words and tiles, byte for byte.  The one exception
-allowed is the certification bound W of the Jones tiles (kJBlockW, kJBlockWsum), which takes
-hypot on each side's libm: within 1e-14 relative (measured: 5 ulp).  Also records the scene-creation time of both builds
+allowed is the certification bound W of the Jones tiles (kJBlockW, and its sum in the float slot
+kJBlockF32), which takes hypot on each side's libm: within 1e-14 relative (measured: 5 ulp), and
+the float sum within 1e-6.  Also records the scene-creation time of both builds
 at the reference's default 100x75 FoV grid (MAIN:16-17)."""
 import json
 import os
@@ -15,7 +16,7 @@ torch = pytest.importorskip("torch")
 pytestmark = pytest.mark.gpu
 
 RESULTS = os.environ.get("WGRT_RESULTS_DIR", os.path.join(os.path.dirname(os.path.dirname(__file__)), "gpurun_out"))
-KJ_HEADER, KJ_BLOCK, KJ_W, KJ_WSUM = 16, 48, 40, 3
+KJ_HEADER, KJ_BLOCK, KJ_W, KJ_F32 = 16, 48, 40, 2
 
 
 @pytest.fixture(scope="module")
@@ -40,12 +41,13 @@ def _scene(geom, luts, host, wavelength=None):
 
 
 def _w_mask(jd):
-    m = np.zeros(jd, bool)
+    """(W[k] doubles, the {Wsum, cosA_2} float pair) of every Jones block"""
+    m, f = np.zeros(jd, bool), np.zeros(jd, bool)
     for b in range((jd - KJ_HEADER) // KJ_BLOCK):
         o = KJ_HEADER + KJ_BLOCK * b
         m[o + KJ_W:o + KJ_W + 3] = True
-        m[o + KJ_WSUM] = True
-    return m
+        f[o + KJ_F32] = True
+    return m, f
 
 
 @pytest.mark.parametrize("nx,ny,profile,wl", [(3, 3, "default", None), (21, 21, "default", None),
@@ -63,9 +65,12 @@ def test_device_scene_equals_host_build(lib, nx, ny, profile, wl):
         np.testing.assert_array_equal(dev.debug_copy("cells"), hst.debug_copy("cells"))
         assert dev.debug_copy("tiles").tobytes() == hst.debug_copy("tiles").tobytes()
         jd, jh = dev.debug_copy("jtiles"), hst.debug_copy("jtiles")
-        w = _w_mask(jd.shape[1])
-        assert jd[:, ~w].tobytes() == jh[:, ~w].tobytes()
+        w, f = _w_mask(jd.shape[1])
+        assert jd[:, ~(w | f)].tobytes() == jh[:, ~(w | f)].tobytes()
         np.testing.assert_allclose(jd[:, w], jh[:, w], rtol=1e-14, atol=0)
+        fd, fh = np.ascontiguousarray(jd[:, f]).view(np.float32), np.ascontiguousarray(jh[:, f]).view(np.float32)
+        np.testing.assert_array_equal(fd[:, 1::2], fh[:, 1::2])            # cosA_2: exact
+        np.testing.assert_allclose(fd[:, 0::2], fh[:, 0::2], rtol=1e-6, atol=0)   # Wsum
     finally:
         dev.close()
         hst.close()
