@@ -587,9 +587,6 @@ struct JLane {
 
 enum : int { kUncertain = -3, kOut = -4 };
 
-#ifndef WGRT_EARLY_MOVE
-#define WGRT_EARLY_MOVE 1
-#endif
 
 // The Jones-vector lane combines per-lane predicates with & and | on purpose: no short-circuit,
 // so the decision is straight-line code instead of nested divergent branches.
@@ -624,17 +621,6 @@ __device__ __forceinline__ bool lane_init(const TraceArgs &A, int64_t i, JLane &
     L.bounces = 1;
     L.pf = 0ull;
     return ok;
-}
-
-__device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, JLane &L, const uint64_t *granule = nullptr,
-                                          uint64_t *gword = nullptr) {
-    const int64_t ld = i;
-    const float *const cl = KA(l);
-    const float fm = KA(m)[ld], fn = KA(n)[ld], fl = cl ? cl[ld] : 0.0f;
-    const float fx = KA(x)[ld], fy = KA(y)[ld], fte = KA(te)[ld], ftm = KA(tm)[ld], d = KA(dph)[ld];
-    const uint32_t rs = KA(rng)[ld];
-    if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return lane_init(A, i, L, fx, fy, fm, fn, fl, fte, ftm, d, rs);
 }
 
 // Ray columns staged in LDS a work-queue chunk at a time: the wave that dequeues a chunk of
@@ -846,12 +832,10 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
     const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double4 cw = block_cw(B);
-#if WGRT_EARLY_MOVE
     // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
     // issued together with its matrix, one memory round trip per interaction less
     const double2 mva = *(const double2 *)(T + kJGap + ga);
     const double2 mvb = *(const double2 *)(T + kJGap + gb);
-#endif
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     if (r.hops) {
         const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
@@ -882,17 +866,15 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     if (code != 0) return code;
     const bool ba = d.s0;
     const int b = ba ? 0 : 1;
-#if WGRT_EARLY_MOVE
+    // the taken branch's new position and its cell word (read by the next pass's advance(); kind
+    // 0: below), issued together with the load of its double-precision matrix.  Only the taken
+    // branch's cell word: loading both candidates' before the decision hid no more latency and
+    // doubled the cell-word gathers (random 4-B reads of a 71 MB grid): 9-12 % slower on C3
     const double2 mv = ba ? mva : mvb;
     r.x = r.x + mv.x;
     r.y = r.y + mv.y;
-    L.pf = locate_c(loc, r.x, r.y);   // read by the next pass's advance() (kind 0: below)
+    L.pf = locate_c(loc, r.x, r.y);
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
-#else
-    // the taken branch: its double-precision matrix and its move, loaded now (L1 / L2-hot)
-    const double2 mv = *(const double2 *)(T + kJGap + (ba ? ga : gb));
-    const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
-#endif
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
@@ -907,19 +889,8 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     if (SINGLE) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
-#if !WGRT_EARLY_MOVE
-    r.x = r.x + mv.x;
-    r.y = r.y + mv.y;
-#endif
     r.gx = mv.x;
     r.gy = mv.y;
-    // the new position's cell word, read by the next pass's advance().  Only the taken
-    // branch's: issuing both candidates' before the decision hid this load's latency but doubled
-    // the cell-word gathers, and those (random 4-B reads of a 71 MB grid, L2 misses) are what the
-    // passes queue behind -- loading one after the decision measured 11 % faster on C3
-#if !WGRT_EARLY_MOVE
-    L.pf = locate_c(loc, r.x, r.y);
-#endif
     if (kind == 0) {
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;

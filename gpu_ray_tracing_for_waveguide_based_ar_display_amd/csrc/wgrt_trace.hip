@@ -53,11 +53,8 @@ double g_cell_mm = [] {
     const char *v = getenv("WGRT_CELL_MM");
     return v ? atof(v) : 0.0078125;   // 1/128 mm: 71 MB grid at C3; fewer EDGE-cell exact tests (fastest on C3)
 }();
-// Ray columns staged in LDS per work-queue chunk (wgrt_device.h stage_chunk); 0: per-lane loads
-#ifndef WGRT_STAGE
-#define WGRT_STAGE 1
-#endif
-// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK; at most 64 when staged)
+// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK; at most 64: a chunk is
+// staged one ray per lane, wgrt_device.h stage_chunk)
 #ifndef WGRT_JCHUNK_DEFAULT
 #define WGRT_JCHUNK_DEFAULT 64
 #endif
@@ -254,7 +251,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         c = ((r / kStripe) * kHeads + x) * kStripe + r % kStripe;
         return true;
     };
-#if WGRT_STAGE
     // this wave's two LDS buffers of staged ray columns (wgrt_device.h stage_chunk): a refill takes
     // rays of at most two chunks, the one being used up and the next
     __shared__ uint32_t stage_buf[4][2][kStageCols * 64];
@@ -264,20 +260,15 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     // ranges of at most 64 rays.
     int sb = 0;
     uint32_t sbase = 0, sbase_prev = 0;
-#endif
     // start the trace (L.i, L.k) on this lane: active, waiting (previous trace still running) or
     // skipped (bad ray / ray already handed to the replay)
     auto start = [&]() {
         uint64_t w = 0;
-#if WGRT_STAGE
         const uint32_t oc = L.i - sbase;
         const bool in_cur = oc < 64u;
         const bool ok = lane_load_staged(A, sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
                                          (int)(in_cur ? oc : L.i - sbase_prev), L.i, L,
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
-#else
-        const bool ok = lane_load(A, L.i, L, (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
-#endif
         waiting = false;
         active = false;
         if (!ok) {
@@ -352,14 +343,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // launch idle lanes are cheap (the next trace's rays keep the chip full): -4 % per trace
         // on C3; single-trace launches gained nothing measurable from batching
         if (FUSED && __popcll(need) < kFusedRefill && __ballot(active || waiting) != 0ull) need = 0ull;
-#if WGRT_STAGE
-        int staged = 0;                // chunks staged by this refill (at most 2: two buffers)
-#endif
+        int staged = 0;                // chunks staged by this refill (at most 1, see below)
         while (need != 0ull && !exhausted) {
             if (cur >= end) {
-#if WGRT_STAGE
-                if (staged == 2) break;   // both buffers hold rays this refill hands out
-#endif
+                // the lanes this refill fills read the current item's buffer and the new one's: a
+                // second new item would overwrite rays not yet read
+                if (staged == 1) break;
                 // dequeue an item when it is needed.  Claiming the next item ahead (to hide the
                 // atomic's latency) doubled the rays a wave holds when the queue runs dry, and the
                 // launch's tail with them: single launches ran 3 % slower with it
@@ -391,13 +380,11 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 const int64_t nr = KA(n_rays);
                 end = cur + chunk < nr ? cur + chunk : nr;
                 cur_k = k;
-#if WGRT_STAGE
                 sb ^= 1;
                 sbase_prev = sbase;
                 sbase = (uint32_t)cur;
                 ++staged;
                 if (lane < (int)(end - cur)) stage_chunk(A, sbufs + sb * (kStageCols * 64), cur + lane);
-#endif
             }
             const int want = __popcll(need);
             const int64_t avail = end - cur;
@@ -415,9 +402,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         // the rays taken from every item of this refill start together: one round trip for
         // their columns however many items they came from
-#if WGRT_STAGE
         if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
-#endif
         if (taken) {
             start();
             taken = false;
@@ -1112,7 +1097,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.part = sc->part;
     A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
     // chunk_order is given in 64-ray chunks; a staged chunk is one ray per lane
-    const int jchunk = A.order ? kChunk : (WGRT_STAGE ? std::min(g_jchunk, 64) : g_jchunk);
+    const int jchunk = A.order ? kChunk : std::min(g_jchunk, 64);
     const dim3 g3((unsigned)grid), b3(256);
     // instantiations: cell word width x fused chain x single-wavelength guard
 #define WGRT_LAUNCH_JONES(CELL, LOCV)                                                                              \
