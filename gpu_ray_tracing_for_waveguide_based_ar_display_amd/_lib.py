@@ -19,7 +19,7 @@ ABI_VERSION = 2
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
             "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
             "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline", "wgrt_debug_set_cert_tol32",
-            "wgrt_debug_set_host_scene", "wgrt_debug_scene_copy",
+            "wgrt_debug_set_host_scene", "wgrt_debug_scene_copy", "wgrt_debug_set_chunk",
             "wgrt_status_string",
             "wgrt_last_error", "wgrt_abi_version")
 
@@ -142,6 +142,9 @@ def load(path: str = LIB_PATH):
         L.wgrt_debug_set_host_scene.argtypes = [ctypes.c_int]
         L.wgrt_debug_scene_copy.restype = st
         L.wgrt_debug_scene_copy.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int64]
+    if hasattr(L, "wgrt_debug_set_chunk"):
+        L.wgrt_debug_set_chunk.restype = ctypes.c_int
+        L.wgrt_debug_set_chunk.argtypes = [ctypes.c_int]
     if hasattr(L, "wgrt_debug_set_cert_tol32"):
         L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
         L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]

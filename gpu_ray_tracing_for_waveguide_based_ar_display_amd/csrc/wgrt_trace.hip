@@ -1299,6 +1299,12 @@ wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int
     return WGRT_OK;
 }
 
+int wgrt_debug_set_chunk(int rays) {
+    const int prev = g_jchunk;
+    if (rays > 0) g_jchunk = std::min(rays, 64);
+    return prev;
+}
+
 void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves) {
     g_timeline = n_waves > 0 ? buf : nullptr;
     g_timeline_waves = n_waves > 0 ? n_waves : 0;

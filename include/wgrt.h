@@ -269,6 +269,11 @@ wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, in
  * buf = NULL or n_waves = 0 turns it off (the default). */
 void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves);
 
+/* Test hook (process-wide): rays per work-queue item of the Jones-vector variants (default 64,
+ * at most 64: an item is staged one ray per lane).  Smaller items make a refill span several
+ * items; results unchanged.  Returns the previous value (a value <= 0 only queries). */
+int wgrt_debug_set_chunk(int rays);
+
 /* Debug hook (process-wide): scenes created while set are built entirely on the host (cell
  * words and tiles by the same rules, host code) instead of on the device; returns the previous
  * setting.  The host build is the reference the device build is checked against. */
