@@ -504,8 +504,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
 // Variants 7 / 9: the persistent loop over the Jones-vector path (32-bit cell words; 64-bit
 // cell words for scenes of more than 16 polygons).  Waves per SIMD: 4 (<= 128 VGPRs, no spills).
-// With the staged ray columns the full-colour single-trace kernel spills 76 B per lane at 96
-// VGPRs (5 waves) and runs 4 % slower than at 4; WGRT_JONES_WAVES=5 builds it so.
+// At 96 VGPRs (5 waves) the full-colour single-trace kernel spills 88 B per lane and runs 36 %
+// slower than at 4; WGRT_JONES_WAVES=5 builds it so.
 #ifndef WGRT_JONES_WAVES
 #define WGRT_JONES_WAVES 4
 #endif
