@@ -9,20 +9,23 @@ One step = one trace of every ray of the batch = ONE launch of the reference's k
 (gpu_ray_tracing_pro_fullColor.py:169-177 issues num_iter = 4 of them, each starting from
 the RNG states the previous one left and adding its out-couplings to the eyebox grid).  The
 headline ``value`` times K such steps as K separate launches (``num_iter = 1`` each, SURVEY.md
-§8(d)), inputs already resident in HBM, plus the RCCL reduce of the eyebox grid at N > 1.
-Two more rates of the same batch ride along: ``main_job`` -- the reference's job shape, 4
-chained traces issued as one call (the engine fuses them into one persistent launch,
-bit-identical to 4 launches) -- and ``fused`` -- all K steps in one call.
+§8(d)), inputs already resident in HBM, plus the eyebox collective at N > 1.  Two more rates of
+the same batch ride along: ``main_job`` -- the reference's job shape, 4 chained traces issued as
+one call (the engine fuses them into one persistent launch, bit-identical to 4 launches) -- and
+``fused`` -- all K steps in one call.
 
-Workloads (``--config``, BASELINE.json configs):
-    C3  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 1024           (1 GPU)
-    C4  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 4096, sharded  (N GPUs)
-    C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce LUT, sharded
-    auto (default): C3 at N = 1, C4 at N > 1 (BASELINE's multi-GPU config); sharded configs
-    split the FoV x wavelength blocks over the ranks (total work fixed: "strong" scaling).
-Multi-GPU: one process per GPU through distributed.py (the same sharding / stepping / reduce
-code the reference-flow driver uses):
+Workloads (``--config``, BASELINE.json configs, configs.py):
+    C2  single-lambda 532 nm, 11x11 FoV, num_rays_per_FoV = 1024
+    C3  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 1024 (the metric's workload)
+    C4  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 4096
+    C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce stress
+    auto (default) = C3 at every N: the metric traces one fixed workload at 1/2/4/8 GPUs, split
+    over the ranks ("strong" scaling); C4 / C5 give their own curves when named.
+Multi-GPU: one process per GPU through distributed.py (interleaved FoV x wavelength blocks, the
+eyebox slabs gathered to rank 0 -- the same code the reference-flow driver uses):
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
+``--emulate-ranks N`` times each of N ranks' shards in turn on one GPU (no collective) and prints
+the per-rank step times and their maximum: the predicted N-GPU step time without the gather.
 """
 from __future__ import annotations
 
@@ -40,16 +43,7 @@ sys.path.insert(0, REPO)
 
 ALGO_BYTES_PER_BOUNCE = 72      # read + write of the minimal 36-B ray record
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
-
-CONFIGS = {
-    "C3": dict(nx=21, ny=21, lambdas=(0, 1, 2), R=1024, profile="default",
-               name="BASELINE config 3: full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV=1024"),
-    "C4": dict(nx=21, ny=21, lambdas=(0, 1, 2), R=4096, profile="default",
-               name="BASELINE config 4: full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV=4096, FoV x lambda sharded"),
-    "C5": dict(nx=41, ny=41, lambdas=(0, 1, 2), R=16384, profile="deep",
-               name="BASELINE config 5: full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV=16384, deep-bounce LUT, "
-                    "FoV x lambda sharded"),
-}
+LIFETIME_BUCKETS = (1, 10, 30, 100, 300, 1000)   # bounce-count histogram edges (last bucket open)
 
 
 def parse(argv=None):
@@ -57,9 +51,16 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="auto", choices=["auto", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="auto", choices=["auto", "C2", "C3", "C4", "C5"])
     ap.add_argument("--lut-seed", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
+    ap.add_argument("--assign", default="interleaved", choices=["interleaved", "contiguous"],
+                    help="FoV x wavelength blocks per rank (distributed.rank_blocks)")
+    ap.add_argument("--collective", default="gather", choices=["gather", "reduce"],
+                    help="eyebox collection at N > 1: gather each rank's own slabs (1/N of the grid per rank) "
+                         "or sum-reduce the whole grid")
+    ap.add_argument("--emulate-ranks", type=int, default=0, metavar="N",
+                    help="one GPU: time each of N ranks' shards in turn (predicted N-GPU step time)")
     ap.add_argument("--no-extras", action="store_true", help="skip the main_job / fused rates")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
@@ -70,18 +71,16 @@ def parse(argv=None):
     ap.add_argument("--cpu-seconds", type=float, default=10.0, help="target CPU-baseline sample length")
     ap.add_argument("--traffic-json", default=os.path.join(REPO, "profiles", "traffic.json"),
                     help="PMC traffic per bounce (tools/pmc_traffic.py), used when its library hash matches")
+    ap.add_argument("--pmc-json", default=os.path.join(REPO, "profiles", "pmc.json"),
+                    help="PMC issue counters per bounce (tools/pmc_summary.py), used when its library hash matches")
     return ap.parse_args(argv)
 
 
-def config_for(name: str, world: int) -> tuple[str, dict]:
+def config_for(name: str, world: int):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS
     if name == "auto":
-        name = "C3" if world == 1 else "C4"
+        name = "C3"
     return name, CONFIGS[name]
-
-
-def metric_name(cfg: dict) -> str:
-    return (f"ray-bounces/sec, full-color {cfg['nx']}x{cfg['ny']} FoV, num_rays_per_FoV={cfg['R']}"
-            + ("" if cfg["profile"] == "default" else f", {cfg['profile']}-bounce LUT"))
 
 
 def lib_sha16() -> str:
@@ -90,24 +89,50 @@ def lib_sha16() -> str:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 
+def lifetime_histogram(per_ray) -> dict:
+    """Per-ray bounce counts of one trace -> mean, max and counts per LIFETIME_BUCKETS bucket."""
+    b = per_ray.cpu().numpy().view(np.uint32).astype(np.int64)
+    edges = list(LIFETIME_BUCKETS) + [np.iinfo(np.int64).max]
+    counts = {f"[{lo},{'inf' if hi == edges[-1] else hi})": int(((b >= lo) & (b < hi)).sum())
+              for lo, hi in zip(edges[:-1], edges[1:])}
+    return {"mean": round(float(b.mean()), 3) if b.size else 0.0, "max": int(b.max()) if b.size else 0,
+            "rays": int(b.size), "by_bounces": counts}
+
+
+def pmc_roofline(path: str, key: str, sha: str):
+    """The issue-side (VALU) roofline of the trace kernel from a PMC summary of this build
+    (tools/pmc_summary.py), or None when no summary matches the library hash."""
+    try:
+        with open(path) as f:
+            ent = json.load(f).get(key)
+    except (OSError, ValueError):
+        return None
+    if not ent or ent.get("lib_sha16") != sha:
+        return None
+    return {k: ent[k] for k in ("valu_busy_frac", "lanes_active_per_valu", "valu_per_bounce", "salu_per_bounce",
+                                "vmem_per_bounce", "wait_any_frac", "effective_clock_ghz", "note") if k in ent}
+
+
 def main(argv=None):
     a = parse(argv)
     import torch
     import torch.distributed as dist
 
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
-                                                                                make_shard, run_steps, split_calls,
-                                                                                timed_run)
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, reserve
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import build_inputs
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (EyeboxGather, hip_shard_builder,
+                                                                                hip_tracer, make_shard,
+                                                                                reduce_eyebox, run_steps,
+                                                                                split_calls, timed_run)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, check_stats, new_stats, reserve,
+                                                                           trace_fullcolor)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != a.gpus:
         raise SystemExit(f"--gpus {a.gpus} but WORLD_SIZE={world}")
+    if a.emulate_ranks and world != 1:
+        raise SystemExit("--emulate-ranks runs on one GPU (WORLD_SIZE=1)")
     if a.one_device:
         if a.dist_backend != "gloo":
             raise SystemExit("--one-device needs --dist-backend gloo (RCCL refuses two ranks on one GPU)")
@@ -120,36 +145,52 @@ def main(argv=None):
         else:
             dist.init_process_group("gloo")
 
-    cname, cfg = config_for(a.config, world)
-    nx, ny, lambdas, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
-    geom = design_geometry(nx, ny)
-    luts = synthetic_luts(geom, seed=a.lut_seed, profile=cfg["profile"])
-    points = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))   # same on every rank
+    cname, w = config_for(a.config, world)
+    nx, ny, lambdas, R = w.nx, w.ny, list(w.lambdas), w.R
+    geom, luts, points = build_inputs(w, lut_seed=a.lut_seed)   # same on every rank (seeded)
     t_scene = time.perf_counter()
     scene = Scene.from_geometry(geom, luts, device=local)
     t_scene = time.perf_counter() - t_scene
-    shard = make_shard(nx, ny, len(lambdas), R, world, rank)
-    rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard.block_lo, shard.block_hi)
+    if a.emulate_ranks:
+        emulate(a, cname, w, scene, points, dev)
+        scene.close()
+        return
+    shard = make_shard(nx, ny, len(lambdas), R, world, rank, a.assign)
+    rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stats = new_stats(dev)
     tracer = hip_tracer(scene, a.variant, stats)
     reserve(scene, shard.n_rays, max(split_calls(max(a.steps, 4), 0)))
+    if world > 1 and a.collective == "gather":
+        all_blocks = [make_shard(nx, ny, len(lambdas), R, world, r, a.assign).blocks for r in range(world)]
+        collect = EyeboxGather(all_blocks, nx, ny, lambdas, scene.num_lmd, device=dev)
+    else:
+        collect = reduce_eyebox
 
     def timed(steps, per_call):
         """steps chained traces as calls of per_call traces (distributed.timed_run: barrier, sync,
-        trace, eyebox reduce, sync, barrier; time MAX and bounces SUM over ranks), with HIP events
-        around every call on the stream the kernels run on (torch's current stream)."""
+        trace, eyebox collective, sync, barrier; time MAX and bounces SUM over ranks), with HIP
+        events around every call on the stream the kernels run on (torch's current stream)."""
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in split_calls(steps, per_call)]
         hook = lambda j, what: ev[j][0 if what == "start" else 1].record()
-        elapsed, b_total, b_local = timed_run(tracer, rays, rng, eb, shard.gid_offset, steps, per_call, stats,
-                                              sync=torch.cuda.synchronize, hook=hook)
+        elapsed, b_total, b_local = timed_run(tracer, rays, rng, eb, shard.gid, steps, per_call, stats,
+                                              sync=torch.cuda.synchronize, hook=hook, collect=collect)
+        check_stats(stats)
         return elapsed, b_total, b_local, [s.elapsed_time(e) for s, e in ev]
 
-    # warm-up: W separate launches (and one fused call, so the fused kernels are loaded too)
-    run_steps(tracer, rays, rng, eb, shard.gid_offset, a.warmup, 1)
+    # warm-up: W separate launches (and one fused call, so the fused kernels are loaded too); the
+    # first one records the per-ray lifetimes of a trace
+    per_ray = torch.zeros(shard.n_rays, dtype=torch.int32, device=dev)
+    if shard.n_rays:
+        g = shard.gid
+        kw = dict(gid_offset=g.offset) if g.offset is not None else dict(
+            gid_blocks=torch.as_tensor(g.block_gid, device=dev), gid_block_rays=R)
+        trace_fullcolor(scene, rays, rng, eb, per_ray_bounces=per_ray, variant=a.variant, **kw)
+    lifetimes = lifetime_histogram(per_ray)
+    run_steps(tracer, rays, rng, eb, shard.gid, max(a.warmup - 1, 0), 1)
     if not a.no_extras:
-        run_steps(tracer, rays, rng, eb, shard.gid_offset, 2, 0)
+        run_steps(tracer, rays, rng, eb, shard.gid, 2, 0)
     torch.cuda.synchronize()
     elapsed, bounces_total, bounces_local, call_ms = timed(a.steps, 1)
     value = bounces_total / elapsed
@@ -176,31 +217,36 @@ def main(argv=None):
                                 "bytes; Infinity-Cache hits included, so an upper bound on HBM bytes), per launch")
         except (OSError, ValueError, KeyError):
             pass
+        valu = pmc_roofline(a.pmc_json, f"{cname}:v{a.variant}", sha)
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_note": traffic_note,
                     "kernel": kernel_name(a.variant, scene), "launch_avg_ms": round(kavg_s * 1e3, 4),
                     "algo_bytes_per_bounce": ALGO_BYTES_PER_BOUNCE,
                     "bounces_per_launch": int(round(bounces_local / len(call_ms))),
+                    "valu": valu if valu is not None else {
+                        "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
                     "note": "launch_avg_ms: HIP events around each launch (trace kernel + its eyebox/replay "
-                            "epilogue kernels) on rank 0"}
+                            "epilogue kernel) on rank 0; valu: the issue-side bound SURVEY.md §8(d) calls binding "
+                            "(VALU busy = SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(geom, luts, points, nx, ny, lambdas, R, a.cpu_seconds)
+        par = f"fov-lambda block shards x{world} ({a.assign})"
+        if world > 1:
+            coll = "gather of own eyebox slabs" if a.collective == "gather" else "reduce(EB)"
+            par += (f" + RCCL {coll}" if a.dist_backend == "nccl" else
+                    f" + gloo {coll}, rehearsal" + (" on one GPU" if a.one_device else ""))
         line = {
-            "metric": metric_name(cfg),
+            "metric": w.metric(),
             "value": round(value, 1), "unit": "ray-bounces/s", "n_gpus": world, "steps": a.steps,
             "warmup": a.warmup, "ms_per_step": round(elapsed / a.steps * 1e3, 4), "higher_is_better": True,
             "scaling": "strong", "vs_baseline": None, "dtype": "f64",
             "data": "synthetic (seeded LUT and ray origins; geometry from the couplers_coor restatement)",
-            "config": {"workload": f"{cname}: {cfg['name']}", "nx": nx, "ny": ny, "lambdas": lambdas,
-                       "num_rays_per_FoV": R, "rays_total": nx * ny * len(lambdas) * R, "rays_rank0": shard.n_rays,
-                       "lut": f"synthetic seed {a.lut_seed} profile {cfg['profile']}",
-                       "parallelism": f"fov-lambda block shards x{world}" + (
-                           (" + RCCL reduce(EB)" if a.dist_backend == "nccl" else
-                            " + gloo reduce(EB), rehearsal" + (" on one GPU" if a.one_device else ""))
-                           if world > 1 else ""),
-                       "kernel_variant": a.variant, "steps_per_launch": 1, "lib_sha16": sha,
-                       "scene_create_s": round(t_scene, 3)},
+            "config": {"workload": f"{cname}: {w.name}", "nx": nx, "ny": ny, "lambdas": lambdas,
+                       "num_rays_per_FoV": R, "rays_total": w.n_rays, "rays_rank0": shard.n_rays,
+                       "lut": f"synthetic seed {a.lut_seed} profile {w.profile}", "gap_scale": w.gap_scale,
+                       "parallelism": par, "kernel_variant": a.variant, "steps_per_launch": 1, "lib_sha16": sha,
+                       "scene_create_s": round(t_scene, 3), "lifetimes_rank0": lifetimes},
             "roofline": roofline,
             "main_job": extras.get("main_job"),
             "fused": extras.get("fused"),
@@ -210,6 +256,48 @@ def main(argv=None):
     scene.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def emulate(a, cname, w, scene, points, dev):
+    """--emulate-ranks N: each rank's shard traced alone on this GPU, K single launches each;
+    prints one JSON line with the per-rank ms per step and the predicted N-GPU step time (their
+    maximum; the eyebox collective is not included)."""
+    import torch
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
+                                                                                make_shard, run_steps)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import check_stats, new_stats, reserve
+    N = a.emulate_ranks
+    nx, ny, lambdas, R = w.nx, w.ny, list(w.lambdas), w.R
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    stats = new_stats(dev)
+    tracer = hip_tracer(scene, a.variant, stats)
+    per_rank = []
+    for r in range(N):
+        shard = make_shard(nx, ny, len(lambdas), R, N, r, a.assign)
+        rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard)
+        reserve(scene, shard.n_rays, 1)
+        run_steps(tracer, rays, rng, eb, shard.gid, a.warmup, 1)
+        torch.cuda.synchronize()
+        stats.zero_()
+        t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        t0.record()
+        run_steps(tracer, rays, rng, eb, shard.gid, a.steps, 1)
+        t1.record()
+        torch.cuda.synchronize()
+        check_stats(stats)
+        ms = t0.elapsed_time(t1) / a.steps
+        per_rank.append({"rank": r, "rays": shard.n_rays, "ms_per_step": round(ms, 4),
+                         "bounces_per_step": int(stats[0].item()) // a.steps})
+        del rays, rng
+    worst = max(p["ms_per_step"] for p in per_rank)
+    total = sum(p["bounces_per_step"] for p in per_rank)
+    print(json.dumps({"emulated_ranks": N, "config": f"{cname}: {w.name}", "assign": a.assign,
+                      "steps": a.steps, "per_rank": per_rank,
+                      "predicted_ms_per_step": worst,
+                      "predicted_value": round(total / (worst / 1e3), 1),
+                      "note": "each rank's shard timed alone on one MI355X; predicted N-GPU step = max over ranks, "
+                              "without the eyebox collective"}), flush=True)
 
 
 def kernel_name(variant, scene):

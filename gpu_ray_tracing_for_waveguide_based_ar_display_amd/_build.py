@@ -40,8 +40,9 @@ def _stale() -> bool:
     if not os.path.exists(LIB):
         return True
     t = os.path.getmtime(LIB)
-    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", "wgrt.h"),
-                                                                   os.path.abspath(__file__)]
+    deps = [os.path.join(CSRC, f) for f in SOURCES + HEADERS] + [os.path.join(REPO, "include", h)
+                                                                   for h in ("wgrt.h", "wgrt_debug.h")]
+    deps.append(os.path.abspath(__file__))
     return any(os.path.getmtime(d) > t for d in deps)
 
 

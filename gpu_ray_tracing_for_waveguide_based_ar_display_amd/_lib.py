@@ -15,13 +15,14 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # WGRT_LIB: load another build of the library (A/B measurements of build variants, tools/ab.py)
 LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
 
-ABI_VERSION = 2
-EXPORTED = ("wgrt_scene_create", "wgrt_scene_destroy", "wgrt_scene_get_info", "wgrt_trace_fullcolor",
-            "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex", "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify", "wgrt_locator_classify_host",
-            "wgrt_selftest_math", "wgrt_debug_set_cert_tol", "wgrt_debug_shadow", "wgrt_debug_set_timeline", "wgrt_debug_set_cert_tol32",
-            "wgrt_debug_set_host_scene", "wgrt_debug_scene_copy", "wgrt_debug_set_chunk",
-            "wgrt_status_string",
-            "wgrt_last_error", "wgrt_abi_version")
+ABI_VERSION = 3
+# include/wgrt.h (the drop-in boundary) and include/wgrt_debug.h (test / profiling hooks)
+EXPORTED = ("wgrt_scene_create", "wgrt_scene_create_ex", "wgrt_scene_destroy", "wgrt_scene_get_info",
+            "wgrt_trace_fullcolor", "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex",
+            "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify",
+            "wgrt_locator_classify_host", "wgrt_selftest_math", "wgrt_status_string", "wgrt_last_error",
+            "wgrt_abi_version")
+EXPORTED_DEBUG = ("wgrt_debug_shadow", "wgrt_debug_scene_copy")
 
 
 class WgrtError(RuntimeError):
@@ -58,13 +59,29 @@ class Rays(ctypes.Structure):
 
 class TraceStats(ctypes.Structure):
     _fields_ = [("bounces", ctypes.c_uint64), ("bad_rays", ctypes.c_uint64),
-                ("eyebox_hits", ctypes.c_uint64), ("replayed", ctypes.c_uint64)]
+                ("eyebox_hits", ctypes.c_uint64), ("replayed", ctypes.c_uint64),
+                ("handoff_giveups", ctypes.c_uint64)]
+
+
+STATS_LEN = len(TraceStats._fields_)   # int64 words of a wgrt_trace_stats (torch stats tensors)
+
+
+class DebugOpts(ctypes.Structure):
+    """wgrt_debug_opts (include/wgrt_debug.h): per-call test / profiling overrides."""
+    _fields_ = [("cert_tol", ctypes.c_double), ("cert_tol32", ctypes.c_double), ("chunk_rays", ctypes.c_int),
+                ("timeline", ctypes.c_void_p), ("timeline_waves", ctypes.c_int64),
+                ("fail_after_trace", ctypes.c_int), ("handoff_wait_ticks", ctypes.c_uint64)]
 
 
 class LaunchOpts(ctypes.Structure):
     _fields_ = [("kernel", ctypes.c_int), ("variant", ctypes.c_int), ("workgroups", ctypes.c_int),
                 ("chunk_order", ctypes.c_void_p), ("n_chunk_order", ctypes.c_int64),
-                ("num_iter", ctypes.c_int)]
+                ("num_iter", ctypes.c_int), ("gid_blocks", ctypes.c_void_p), ("gid_block_rays", ctypes.c_int64),
+                ("debug", ctypes.POINTER(DebugOpts))]
+
+
+class SceneOpts(ctypes.Structure):
+    _fields_ = [("cell_mm", ctypes.c_double), ("host_build", ctypes.c_int)]
 
 
 class ShadowStats(ctypes.Structure):
@@ -101,6 +118,9 @@ def load(path: str = LIB_PATH):
     st = ctypes.c_int
     L.wgrt_scene_create.restype = st
     L.wgrt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_int, ctypes.POINTER(_vp)]
+    L.wgrt_scene_create_ex.restype = st
+    L.wgrt_scene_create_ex.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_int, ctypes.POINTER(SceneOpts),
+                                       ctypes.POINTER(_vp)]
     L.wgrt_scene_destroy.restype = st
     L.wgrt_scene_destroy.argtypes = [_vp]
     L.wgrt_scene_get_info.restype = st
@@ -129,27 +149,12 @@ def load(path: str = LIB_PATH):
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
     L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
-    # debug / test hooks: optional, so tools can load older builds of the library (tools/ab.py)
-    if hasattr(L, "wgrt_debug_shadow"):
-        L.wgrt_debug_shadow.restype = st
-        L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
-                                        _vp, _vp, _vp]
-    if hasattr(L, "wgrt_debug_set_timeline"):
-        L.wgrt_debug_set_timeline.restype = None
-        L.wgrt_debug_set_timeline.argtypes = [_vp, ctypes.c_int64]
-    if hasattr(L, "wgrt_debug_set_host_scene"):
-        L.wgrt_debug_set_host_scene.restype = ctypes.c_int
-        L.wgrt_debug_set_host_scene.argtypes = [ctypes.c_int]
-        L.wgrt_debug_scene_copy.restype = st
-        L.wgrt_debug_scene_copy.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int64]
-    if hasattr(L, "wgrt_debug_set_chunk"):
-        L.wgrt_debug_set_chunk.restype = ctypes.c_int
-        L.wgrt_debug_set_chunk.argtypes = [ctypes.c_int]
-    if hasattr(L, "wgrt_debug_set_cert_tol32"):
-        L.wgrt_debug_set_cert_tol32.restype = ctypes.c_double
-        L.wgrt_debug_set_cert_tol32.argtypes = [ctypes.c_double]
-    L.wgrt_debug_set_cert_tol.restype = ctypes.c_double
-    L.wgrt_debug_set_cert_tol.argtypes = [ctypes.c_double]
+    # test / profiling hooks (include/wgrt_debug.h)
+    L.wgrt_debug_shadow.restype = st
+    L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
+                                    _vp, _vp, _vp]
+    L.wgrt_debug_scene_copy.restype = st
+    L.wgrt_debug_scene_copy.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int64]
     L.wgrt_status_string.restype = ctypes.c_char_p
     L.wgrt_status_string.argtypes = [ctypes.c_int]
     L.wgrt_last_error.restype = ctypes.c_char_p
@@ -237,13 +242,16 @@ class Scene:
 
     def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
                  eff_reg_FOV_range, lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2,
-                 lut_TIR, lut_gap, device: int = 0):
+                 lut_TIR, lut_gap, device: int = 0, cell_mm: float = 0.0, host_build: bool = False):
+        """``cell_mm`` / ``host_build``: wgrt_scene_opts (0 / False: the defaults)."""
         L = load()
         desc, _keep, (nl, nx, ny, nfc, noc) = make_desc(
             IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
             lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2, lut_TIR, lut_gap)
         h = _vp()
-        check(L.wgrt_scene_create(ctypes.byref(desc), int(device), ctypes.byref(h)), "wgrt_scene_create")
+        opts = SceneOpts(float(cell_mm), 1 if host_build else 0)
+        check(L.wgrt_scene_create_ex(ctypes.byref(desc), int(device), ctypes.byref(opts), ctypes.byref(h)),
+              "wgrt_scene_create")
         self._h = h
         self.single_lambda = np.ndim(lut_TIR) == 3
         self.device = int(device)
@@ -252,9 +260,10 @@ class Scene:
         self.n_g = float(n_g)
 
     @classmethod
-    def from_geometry(cls, geom, luts: dict, device: int = 0, wavelength: int | None = None):
+    def from_geometry(cls, geom, luts: dict, device: int = 0, wavelength: int | None = None, **opts):
         """Scene of a geometry + LUT set.  ``wavelength=l`` builds the single-wavelength scene
-        of wavelength l (the arrays process_rays_kernel_pro takes, luts.single_wavelength)."""
+        of wavelength l (the arrays process_rays_kernel_pro takes, luts.single_wavelength);
+        ``opts``: ``cell_mm`` / ``host_build`` (wgrt_scene_opts)."""
         tir, gap = geom.lut_TIR, geom.lut_gap
         if wavelength is not None:
             from .luts import single_wavelength
@@ -262,7 +271,7 @@ class Scene:
         return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
                    geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts["lut_ic1"], luts["lut_ic2"],
                    luts["lut_ic3"], luts["lut_fc1"], luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"],
-                   tir, gap, device=device)
+                   tir, gap, device=device, **opts)
 
     @property
     def handle(self):

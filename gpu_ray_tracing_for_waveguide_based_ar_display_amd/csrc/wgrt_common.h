@@ -177,15 +177,21 @@ WGRT_HD bool inside_or_on_edge_subset(double px, double py, const double *xy, in
     return inside;
 }
 
-// xorshift32 (13, 17, 5) of GRTF:25-34; gid is the GLOBAL ray index.
-WGRT_HD double rng_draw(uint32_t &s, int64_t gid) {
+// xorshift32 (13, 17, 5) of GRTF:25-34.  gid() returns the GLOBAL ray index; it is evaluated
+// only for the zero-state fix-up (GRTF:28-29), so a kernel may look it up lazily.
+template <class GidFn>
+WGRT_HD double rng_draw_lazy(uint32_t &s, GidFn gid) {
     uint32_t v = s;
-    if (v == 0u) v = 0x6D2B79F5u ^ (uint32_t)(gid + 1);
+    if (v == 0u) v = 0x6D2B79F5u ^ (uint32_t)(gid() + 1);
     v ^= v << 13;
     v ^= v >> 17;
     v ^= v << 5;
     s = v;
     return (double)v * (1.0 / 4294967296.0);
+}
+
+WGRT_HD double rng_draw(uint32_t &s, int64_t gid) {
+    return rng_draw_lazy(s, [gid]() { return gid; });
 }
 
 }  // namespace wgrt

@@ -66,13 +66,17 @@ struct TraceArgs {
     unsigned long long *other_ctr;      // the next launch's counter set, zeroed by this launch's epilogue
     uint32_t *full_list;                // out-coupling queue blocks the trace waves filled (block numbers)
     unsigned long long *full_count;
-    unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_set_timeline), NULL normally
+    unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_opts), timeline kernels only
     int64_t timeline_waves;
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one
     // launch; rng64[i] = (state << 32) | iter_tag(iter_epoch, traces completed, broken)
     int n_iter;
     uint64_t *rng64;
     uint32_t iter_epoch;
+    unsigned long long handoff_wait_ticks;   // fused: s_memrealtime ticks a lane may wait for a hand-off
+    // global ray ids of an interleaved shard (wgrt_launch_opts.gid_blocks): NULL = gid_offset + i
+    const int64_t *gid_blocks;
+    int64_t gid_block_rays;
 };
 
 // A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
@@ -90,6 +94,20 @@ __device__ __forceinline__ T karg(size_t off) {
 #define KA(f) karg<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
 // the same for the locator's exact-test arrays (TraceArgs::loc holds them for every variant)
 #define KLOC(f) karg<decltype(Locator::f)>(offsetof(TraceArgs, loc) + offsetof(Locator, f))
+
+// Global id of local ray i (wgrt_launch_opts.gid_blocks): only the zero-state RNG fix-up reads it.
+__device__ __forceinline__ int64_t ray_gid(const TraceArgs &A, int64_t i) {
+    return A.gid_blocks ? A.gid_blocks[i / A.gid_block_rays] + i % A.gid_block_rays : A.gid_offset + i;
+}
+// The same from the kernarg segment (kernels whose first parameter is the TraceArgs).
+__device__ __forceinline__ int64_t ray_gid_ka(int64_t i) {
+    const int64_t *gb = KA(gid_blocks);
+    if (gb) {
+        const int64_t r = KA(gid_block_rays);
+        return gb[i / r] + i % r;
+    }
+    return KA(gid_offset) + i;
+}
 
 
 constexpr int kPolyEff1 = 0;
@@ -335,7 +353,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     const bool three = kind >= 3;
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
     const double denom = entry ? T[kTileCosIc1] : r.cos_t;
-    const double u = rng_draw(r.s, A.gid_offset + L.i);
+    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid(A, L.i); });
 
     // Decide the branch.  The reference compares u with cumulative branch efficiencies
     // e_k = (hypot(Ete')^2 + hypot(Etm')^2) * cosA_k / cos(theta) [* or / n_g].  Here the
@@ -586,6 +604,13 @@ struct JLane {
 };
 
 enum : int { kUncertain = -3, kOut = -4 };
+
+// Default bases of the certification bounds (wgrt_debug_opts overrides them per call): the
+// double-precision evaluation's, and the single-precision estimate's -- 8e-6 covers the rounding
+// of |M E|^2 from float matrices and vector (about 26 ulp(1) of the bound's W scale) five times
+// over; wgrt_shadow.hip measures the margin.
+constexpr double kCertTol = 1e-10;
+constexpr double kCertTol32 = 8e-6;
 
 
 // The Jones-vector lane combines per-lane predicates with & and | on purpose: no short-circuit,
@@ -847,7 +872,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
         r.hops = 0;
     }
     const double denom = entry ? cg.x : r.cos_t;
-    const double u = rng_draw(r.s, A.gid_offset + (int64_t)L.i);
+    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka((int64_t)L.i); });
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;

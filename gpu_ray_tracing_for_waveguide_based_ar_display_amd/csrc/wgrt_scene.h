@@ -28,6 +28,7 @@ struct wgrt_scene {
     int64_t tiles = 0;
     int64_t edge_cells = 0;        // locator cells with an EDGE class
     int jones_grid[2][2][2] = {};   // resident 256-thread workgroups: [64-bit cells][fused][single wavelength]
+    int jones_tl_grid[2] = {};      // ... of the debug timeline instantiations (32-bit cells): [fused]
     // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so
     // they may share it; launches on different streams never do)
     struct Scratch {
@@ -35,6 +36,7 @@ struct wgrt_scene {
         // full-block count), used by alternate launches: a launch's epilogue zeroes the other one
         unsigned long long *ctr = nullptr;
         uint32_t parity = 0;                 // the set the next launch uses
+        bool dirty = false;                  // a launch failed half-way: both sets need zeroing
         uint32_t *full = nullptr;            // full-block list (qcap / kQBlock entries)
         uint32_t *list = nullptr;            // replay list
         int64_t cap = 0;                     // replay list entries

@@ -32,6 +32,7 @@
 #include <string>
 
 #include "../../include/wgrt.h"
+#include "../../include/wgrt_debug.h"
 #include "wgrt_common.h"
 #include "wgrt_device.h"
 #include "wgrt_scene.h"
@@ -359,8 +360,8 @@ extern "C" wgrt_status wgrt_debug_shadow(const wgrt_scene *s, const wgrt_rays *r
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
     A.threshold = single ? 1e-15 : 0.0;
-    A.cert_tol = wgrt_debug_set_cert_tol(0.0);   // the bounds the product lane uses now (0: query only)
-    A.cert_tol32 = std::max(wgrt_debug_set_cert_tol32(0.0), A.cert_tol);
+    A.cert_tol = kCertTol;   // the bounds the product lane uses by default
+    A.cert_tol32 = std::max(kCertTol32, A.cert_tol);
     S.out = stats;
     const int64_t blocks = std::min<int64_t>((n_rays + 255) / 256, 16384);
     hipLaunchKernelGGL(shadow_kernel<Locator>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, S, A.loc);

@@ -31,6 +31,7 @@
 #include <vector>
 
 #include "../../include/wgrt.h"
+#include "../../include/wgrt_debug.h"
 #include "wgrt_common.h"
 #include "wgrt_device.h"
 #include "wgrt_scene.h"
@@ -48,29 +49,9 @@ wgrt_status fail(wgrt_status s, const std::string &msg) {
 
 namespace {
 
-// Cell size (mm) of the global-memory locator grid (env WGRT_CELL_MM).
-double g_cell_mm = [] {
-    const char *v = getenv("WGRT_CELL_MM");
-    return v ? atof(v) : 0.0078125;   // 1/128 mm: 71 MB grid at C3; fewer EDGE-cell exact tests (fastest on C3)
-}();
-// rays per work-queue chunk of the Jones-vector variants (env WGRT_JCHUNK; at most 64: a chunk is
-// staged one ray per lane, wgrt_device.h stage_chunk)
-#ifndef WGRT_JCHUNK_DEFAULT
-#define WGRT_JCHUNK_DEFAULT 64
-#endif
-int g_jchunk = [] {
-    const char *v = getenv("WGRT_JCHUNK");
-    const int c = v ? atoi(v) : WGRT_JCHUNK_DEFAULT;
-    return c >= 1 ? c : WGRT_JCHUNK_DEFAULT;
-}();
-double g_cert_tol = 1e-10;   // Jones-vector variants' double-precision certification bound (wgrt_debug_set_cert_tol)
-// ... and the single-precision estimate's (wgrt_debug_set_cert_tol32): 8e-6 covers the rounding of
-// |M E|^2 from float matrices and vector (about 26 ulp(1) of the bound's W scale) five times over;
-// wgrt_shadow.hip measures the margin
-double g_cert_tol32 = 8e-6;
-unsigned long long *g_timeline = nullptr;   // wgrt_debug_set_timeline
-
-int64_t g_timeline_waves = 0;
+// Cell size (mm) of the global-memory locator grid (wgrt_scene_opts.cell_mm = 0): 1/128 mm, a 71 MB
+// grid at C3; fewer EDGE-cell exact tests than coarser grids (fastest on C3).
+constexpr double kDefaultCellMm = 0.0078125;
 
 
 #define HIP_TRY(expr)                                                                       \
@@ -112,11 +93,11 @@ constexpr int kQBlock = WGRT_QBLOCK;    // out-coupling queue slots a wave reser
                                // out-couples ~10 rays per trace)
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
-    __shared__ unsigned long long red[4][3];
+    __shared__ unsigned long long red[4][4];
     const unsigned long long nr = *A.replay_count, nf = *A.full_count;
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
-    uint64_t h = 0, b = 0, bad = 0;
+    uint64_t h = 0, b = 0, bad = 0, gu = 0;
     for (unsigned long long e = tid; e < nf * kQBlock; e += nth) {
         {
             const unsigned long long j = (unsigned long long)A.full_list[e / kQBlock] * kQBlock + e % kQBlock;
@@ -144,6 +125,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
             b += slot[0];
             bad += slot[1];
             h += slot[2];
+            gu += slot[3];
         }
         if (threadIdx.x < kScratchCtr) A.other_ctr[threadIdx.x] = 0ull;
     }
@@ -151,10 +133,12 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     b = wave_sum(b);
     bad = wave_sum(bad);
     h = wave_sum(h);
+    gu = wave_sum(gu);
     if ((threadIdx.x & 63) == 0) {
         red[w][0] = b;
         red[w][1] = bad;
         red[w][2] = h;
+        red[w][3] = gu;
     }
     __syncthreads();
     if (threadIdx.x == 0 && A.stats) {
@@ -162,9 +146,11 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
         const unsigned long long t0 = red[0][0] + red[1][0] + red[2][0] + red[3][0];
         const unsigned long long t1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        const unsigned long long t3 = red[0][3] + red[1][3] + red[2][3] + red[3][3];
         if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
         if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
         if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
+        if (t3) atomicAdd((unsigned long long *)&st->handoff_giveups, t3);
         if (blockIdx.x == 0 && nr) atomicAdd((unsigned long long *)&st->replayed, nr);
     }
 }
@@ -179,11 +165,19 @@ constexpr int kFusedRefill = 16;
 #define WGRT_STRIPE 16
 #endif
 constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
-// Passes a fused-launch lane may wait for its ray's previous trace before it gives the ray up
-// (counted in wgrt_trace_stats.bad_rays).  A legitimate wait is bounded by that trace's length
-// (<= 1e5 + 1 bounces, at least one per pass of the wave running it); the bound only turns a
-// hand-off bug (epoch / tag) into a visible count instead of a hung GPU.
-constexpr uint32_t kMaxWaitPasses = 1u << 24;
+
+// How long a fused-launch lane may wait for its ray's previous trace before it gives the trace
+// up (wgrt_trace_stats.handoff_giveups; the Python layer raises on it).  A legitimate wait for
+// trace k of ray i ends once trace k - 1 of ray i has ended.  Item (k - 1, c) was dequeued from the
+// same head before (k, c) (heads hand out iteration-major), and the wave holding it starts the
+// ray within the lifetime of the rays on its lanes, then traces it: each at most kMaxLoop + 1
+// bounces = passes of that wave, and that wave's lanes may themselves wait on iteration k - 2.
+// With a pass at most ~5 us (bulk C3 passes take 5.8 us / 64 lanes of 4 waves per SIMD, a
+// lone wave's about 3 us) one trace or one start delay is under 0.5 s, so a correct wait
+// is below k * 2 * 0.5 s: the bound is 1 s per chained trace plus 1 s.  It turns a hand-off bug
+// (epoch / tag) into a visible count within seconds instead of a hung GPU; it cannot be ms
+// without failing legitimate 1e5-bounce rays.
+constexpr unsigned long long kHandoffTicksPerIter = 100000000ull;   // s_memrealtime: 100 MHz
 
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
@@ -206,19 +200,21 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
 // (waiting in place, lane idle, until the tag says k) -- the granule hand-off of
 // MI355X_MICROARCH.md's price list, valid whatever the XCD placement.  Results are identical
 // to n_iter launches: each ray's traces run in order from the same states; eyebox adds commute.
-template <bool FUSED, bool SINGLE, class Loc>
+// TL: the debug wave timeline (wgrt_debug_opts.timeline); the product instantiations have TL = false
+// and contain none of its code.
+template <bool FUSED, bool SINGLE, bool TL, class Loc>
 __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, unsigned long long *heads, int chunk) {
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
     int head = xcc_id();
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
-    // debug timeline (wgrt_debug_set_timeline; NULL in production): per wave, start / queue
-    // exhausted / end (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD,
-    // and the passes / lane-passes up to the queue running dry
-    unsigned long long *const tl = KA(timeline);
+    // debug timeline (TL instantiations only): per wave, start / queue exhausted / end
+    // (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD, and the passes /
+    // lane-passes up to the queue running dry
+    unsigned long long *const tl = TL ? KA(timeline) : nullptr;
     const int64_t tl_wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const bool tl_on = tl != nullptr && tl_wave < KA(timeline_waves);
+    const bool tl_on = TL && tl != nullptr && tl_wave < KA(timeline_waves);
     unsigned long long tl_passes = 0, tl_lanes = 0;
     if (tl_on && lane == 0) tl[8 * tl_wave] = __builtin_amdgcn_s_memrealtime();
     uint32_t cur_k = 0;               // the item's iteration
@@ -229,8 +225,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     bool entry = false;
     // per-lane totals in 32 bits: a lane's bounce total is added to the stats directly before it
     // could overflow (2^31 bounces on one lane: never in practice)
-    uint32_t tot_b = 0, tot_bad = 0;
-    uint32_t wait_passes = 0;          // fused: passes spent waiting for the current ray
+    uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0;
+    unsigned long long wait_t0 = 0;    // fused: when this lane started waiting for its ray (s_memrealtime)
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
     bool qblk = false;                 // a block has been reserved
@@ -283,7 +279,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 return;   // abandoned in an earlier iteration: the replay kernel finishes it
             } else {
                 waiting = true;
-                wait_passes = 0;
+                wait_t0 = __builtin_amdgcn_s_memrealtime();
                 return;
             }
         }
@@ -332,9 +328,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 entry = true;
             } else if ((tag >> 8) == ((A.iter_epoch << 1) | 1u)) {
                 waiting = false;   // abandoned in an earlier iteration: the replay kernel finishes it
-            } else if (++wait_passes > kMaxWaitPasses) {
-                waiting = false;   // hand-off never arrived: give the ray up, visibly
-                ++tot_bad;
+            } else if (__builtin_amdgcn_s_memrealtime() - wait_t0 > A.handoff_wait_ticks) {
+                waiting = false;   // hand-off never arrived: give the trace up, visibly
+                ++tot_giveup;
             }
         }
         uint64_t need = __ballot(!active && !waiting);
@@ -367,7 +363,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 }
                 if (!got) {
                     exhausted = true;
-                    if (tl_on && lane == 0) {
+                    if (TL && tl_on && lane == 0) {
                         tl[8 * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
                         tl[8 * tl_wave + 6] = tl_passes;
                         tl[8 * tl_wave + 7] = tl_lanes;
@@ -408,7 +404,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             taken = false;
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
-        if (tl_on) {
+        if (TL && tl_on) {
             ++tl_passes;
             tl_lanes += __popcll(__ballot(active));
         }
@@ -476,21 +472,23 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             tot_h = eyebox_add(A, el, em, en, px, py) ? 1u : 0u;
         }
     }
-    if (tl_on && lane == 0) {
+    if (TL && tl_on && lane == 0) {
         tl[8 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
         tl[8 * tl_wave + 3] = tl_passes;
         tl[8 * tl_wave + 4] = tl_lanes;
         tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
     }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
-    __shared__ unsigned long long red[4][3];
+    __shared__ unsigned long long red[4][4];
     const uint64_t sum_b = wave_sum((uint64_t)tot_b);
     const uint64_t sum_bad = wave_sum((uint64_t)tot_bad);
     const uint64_t sum_h = wave_sum((uint64_t)tot_h);
+    const uint64_t sum_g = FUSED ? wave_sum((uint64_t)tot_giveup) : 0ull;
     if (lane == 0) {
         red[threadIdx.x >> 6][0] = sum_b;
         red[threadIdx.x >> 6][1] = sum_bad;
         red[threadIdx.x >> 6][2] = sum_h;
+        red[threadIdx.x >> 6][3] = sum_g;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
@@ -498,7 +496,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
         slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
-        slot[3] = 0;
+        slot[3] = red[0][3] + red[1][3] + red[2][3] + red[3][3];
     }
 }
 
@@ -516,7 +514,15 @@ constexpr int jones_waves() {
 template <class CellT, bool FUSED, bool SINGLE>
 __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    jones_body<FUSED, SINGLE>(A, loc, counter, chunk);
+    jones_body<FUSED, SINGLE, false>(A, loc, counter, chunk);
+}
+
+// The same loop with the debug wave timeline (wgrt_debug_opts.timeline; tools/timeline.py): a
+// separate instantiation, so the product kernels carry none of its code.
+template <class CellT, bool FUSED, bool SINGLE>
+__global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_tl_kernel(
+    TraceArgs A, LocatorT<CellT> loc, unsigned long long *counter, int chunk) {
+    jones_body<FUSED, SINGLE, true>(A, loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -674,11 +680,6 @@ __global__ __launch_bounds__(64) void pack_tiles_kernel(PackView v, int64_t ntil
 
 namespace {
 
-bool g_host_scene = [] {   // wgrt_debug_set_host_scene / env WGRT_SCENE_HOST=1: build scenes on the host
-    const char *v = getenv("WGRT_SCENE_HOST");
-    return v && atoi(v) != 0;
-}();
-
 // hipMalloc + copy of n elements (n may be 0)
 template <class T>
 wgrt_status upload_n(const T *src, size_t n, T **dst) {
@@ -713,16 +714,23 @@ wgrt_status upload(const std::vector<T> &v, T **dst) {
 extern "C" {
 
 wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scene **out) {
+    return wgrt_scene_create_ex(desc, device, nullptr, out);
+}
+
+wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const wgrt_scene_opts *opts,
+                                 wgrt_scene **out) {
     if (!desc || !out) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL desc / out");
     *out = nullptr;
     const wgrt_scene_desc &d = *desc;
+    const double cell_mm = (opts && opts->cell_mm > 0.0) ? opts->cell_mm : kDefaultCellMm;
+    if (opts && !(opts->cell_mm >= 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be >= 0");
+    const bool host_build = opts && opts->host_build != 0;
     // host: validation, the locator's geometry (extent, vertices, row bands) and the trig table
     // (every cos / sin on the host libm); the cell words and the tiles are built on the device
-    // (wgrt_debug_set_host_scene: both on the host, the reference build the device one is
-    // checked against)
+    // (host_build: both on the host, the reference build the device one is checked against)
     SceneHost host;
     try {
-        build_scene_host(d, g_cell_mm, host, g_host_scene, g_host_scene);
+        build_scene_host(d, cell_mm, host, host_build, host_build);
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
@@ -751,7 +759,7 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         (st = upload(host.loc.bands, &s->d_bands)) != WGRT_OK)
         return bail(st);
     const size_t ncells = (size_t)host.loc.ncx * host.loc.ncy;
-    if (g_host_scene) {
+    if (host_build) {
         if ((st = upload(host.tiles, &s->d_tiles)) != WGRT_OK || (st = upload(host.jtiles, &s->d_jtiles)) != WGRT_OK ||
             (st = upload(host.loc.cells, &s->d_cells)) != WGRT_OK)
             return bail(st);
@@ -849,6 +857,9 @@ wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scen
         WGRT_GRID(uint64_t, 1, true, false);
         WGRT_GRID(uint64_t, 1, true, true);
 #undef WGRT_GRID
+        // the debug timeline instantiations (32-bit cells, full colour, single / fused)
+        HIP_TRY(grid_of((const void *)trace_jones_tl_kernel<uint32_t, false, false>, s->jones_tl_grid[0]));
+        HIP_TRY(grid_of((const void *)trace_jones_tl_kernel<uint32_t, true, false>, s->jones_tl_grid[1]));
     }
     s->loc_host = host.loc;
     s->loc_host.cells.clear();
@@ -906,9 +917,12 @@ namespace {
 
 // The Jones-vector variants' per-stream launch scratch (work-queue heads, replay list,
 // out-coupling queue, fused-launch granules), grown to n_rays x num_iter traces on `grid`
-// workgroups.  Growing synchronises the stream (the old buffers may be in use).  For a fused
-// launch (epoch != NULL) the launch epoch of the granule tags is advanced here, under the same
-// lock, and returned.
+// workgroups.  Growing synchronises the stream (the old buffers may be in use).  For a launch
+// (parity != NULL) the counter set it uses is returned and the next launch is given the other
+// one -- only once every allocation has succeeded, so a failed growth leaves the sets as they
+// were; a launch that fails after this point marks the scratch dirty (mark_dirty), and the next
+// call zeroes both sets before it uses either.  For a fused launch (epoch != NULL) the launch
+// epoch of the granule tags is advanced here, under the same lock, and returned.
 wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num_iter, int64_t grid,
                            wgrt_scene::Scratch **out, uint32_t *epoch = nullptr, uint32_t *parity = nullptr) {
     hipStream_t st = (hipStream_t)stream;
@@ -920,12 +934,20 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
         // the next launch uses
         hipError_t e = hipMalloc((void **)&sc->ctr, 2 * kScratchCtr * sizeof(unsigned long long));
         if (e == hipSuccess) e = hipMemset(sc->ctr, 0, 2 * kScratchCtr * sizeof(unsigned long long));
-        if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+        if (e != hipSuccess) {
+            (void)hipFree(sc->ctr);
+            sc->ctr = nullptr;
+            return fail(WGRT_ERR_HIP, std::string("hipMalloc(scratch): ") + hipGetErrorString(e));
+        }
         sc->parity = 0;
+        sc->dirty = false;
     }
-    if (parity) {   // a launch: its counter set, and the next launch takes the other one
-        *parity = sc->parity;
-        sc->parity ^= 1u;
+    if (sc->dirty) {
+        // an earlier launch failed half-way (its epilogue may not have zeroed the next set)
+        HIP_TRY(hipStreamSynchronize(st));
+        HIP_TRY(hipMemset(sc->ctr, 0, 2 * kScratchCtr * sizeof(unsigned long long)));
+        sc->parity = 0;
+        sc->dirty = false;
     }
     // counter partials: one slot per trace-kernel workgroup
     const int64_t slots = grid;
@@ -986,8 +1008,29 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
         }
         *epoch = sc->iter_epoch;
     }
+    if (parity) {   // a launch: its counter set; the next launch takes the other one
+        *parity = sc->parity;
+        sc->parity ^= 1u;
+    }
     return WGRT_OK;
 }
+
+// A launch failed after ensure_scratch handed it a counter set: neither set can be trusted to be
+// zero any more (see ensure_scratch).
+void mark_dirty(wgrt_scene *ms, wgrt_scene::Scratch *sc) {
+    std::lock_guard<std::mutex> lk(ms->scratch_mu);
+    sc->dirty = true;
+}
+
+struct LaunchCfg {
+    int variant = 0, workgroups = 0, num_iter = 1;
+    bool single = false;
+    const int32_t *chunk_order = nullptr;
+    int64_t n_chunk_order = 0;
+    const int64_t *gid_blocks = nullptr;
+    int64_t gid_block_rays = 0;
+    const wgrt_debug_opts *dbg = nullptr;
+};
 
 // One launch of the bounce kernel.  single: the single-wavelength kernel
 // process_rays_kernel_pro (GRTF:419-831) -- no lmd_num column, wavelength 0 of a
@@ -995,19 +1038,27 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
 // (GRTF:833-1246), threshold 0.  The two kernels differ in nothing else.
 wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
                          uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats, uint32_t *per_ray_bounces,
-                         void *stream, int variant, int workgroups, bool single, const int32_t *chunk_order = nullptr,
-                         int64_t n_chunk_order = 0, int num_iter = 1) {
+                         void *stream, LaunchCfg c) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
+    const bool single = c.single;
+    int variant = c.variant;
+    int num_iter = c.num_iter;
+    const wgrt_debug_opts *dbg = c.dbg;
     if (single && s->nl != 1)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "single-wavelength trace needs a scene built with num_lmd == 1");
     if (variant != 0 && variant != 1 && variant != 7 && variant != 9)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "kernel variant must be 0 (auto), 1, 7 or 9");
     if (num_iter < 1) num_iter = 1;
     if (num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter must be <= 255");
-    if (num_iter > 1 && (per_ray_bounces || chunk_order))
+    if (num_iter > 1 && (per_ray_bounces || c.chunk_order))
         return fail(WGRT_ERR_INVALID_ARGUMENT, "num_iter > 1 takes no per_ray_bounces / chunk_order");
-    if (chunk_order && variant == 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order needs variant 0, 7 or 9");
+    if (c.chunk_order && variant == 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order needs variant 0, 7 or 9");
+    if (c.gid_blocks && (c.gid_block_rays < 1 || gid_offset != 0))
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "gid_blocks needs gid_block_rays >= 1 and gid_offset == 0");
+    if (dbg && (dbg->cert_tol < 0.0 || dbg->cert_tol32 < 0.0 || dbg->chunk_rays < 0 ||
+                (dbg->timeline && dbg->timeline_waves < 0)))
+        return fail(WGRT_ERR_INVALID_ARGUMENT, "bad wgrt_debug_opts");
     if (n_rays == 0) return WGRT_OK;
     if (!rays->x || !rays->y || !rays->m || !rays->n || (!single && !rays->lmd_num) || !rays->te || !rays->tm ||
         !rays->delta_phase || !rng_states || !matrix_EB)
@@ -1016,15 +1067,21 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     if (variant >= 7 && n_rays > 0xffffffffll)
         return fail(WGRT_ERR_UNSUPPORTED, "variants 7 / 9 index at most 2^32 - 1 rays per launch");
     if (variant == 0) variant = n_rays > 0xffffffffll ? 1 : (s->d_cells32 ? 7 : 9);   // auto
+    const bool timeline = dbg && dbg->timeline && dbg->timeline_waves > 0;
+    if (timeline && (variant != 7 || single))
+        return fail(WGRT_ERR_UNSUPPORTED, "the wave timeline is built for the full-colour 32-bit-cell kernel only");
     if (num_iter > 1 && variant == 1) {   // chained launches, as the reference issues them
+        LaunchCfg one = c;
+        one.variant = variant;
+        one.num_iter = 1;
         for (int it = 0; it < num_iter; ++it) {
             const wgrt_status e = trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, nullptr,
-                                               stream, variant, workgroups, single);
+                                               stream, one);
             if (e != WGRT_OK) return e;
         }
         return WGRT_OK;
     }
-    if (chunk_order && n_chunk_order != (n_rays + kChunk - 1) / kChunk)
+    if (c.chunk_order && c.n_chunk_order != (n_rays + kChunk - 1) / kChunk)
         return fail(WGRT_ERR_INVALID_ARGUMENT, "chunk_order must list ceil(n_rays / 64) chunks");
     TraceArgs A{};
     A.x = rays->x;
@@ -1033,7 +1090,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.n = rays->n;
     A.l = single ? nullptr : rays->lmd_num;
     A.threshold = single ? 1e-15 : 0.0;
-    A.order = chunk_order;   // a permutation of the 64-ray chunks (trusted device data)
+    A.order = c.chunk_order;   // a permutation of the 64-ray chunks (trusted device data)
     A.te = rays->te;
     A.tm = rays->tm;
     A.dph = rays->delta_phase;
@@ -1043,6 +1100,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.per_ray = per_ray_bounces;
     A.n_rays = n_rays;
     A.gid_offset = gid_offset;
+    A.gid_blocks = c.gid_blocks;
+    A.gid_block_rays = c.gid_blocks ? c.gid_block_rays : 1;
     A.tiles = s->d_tiles;
     A.loc = make_locator(s);
     A.tile_d = s->tile_d;
@@ -1053,10 +1112,11 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.nl = s->nl;
     A.n_g = s->n_g;
     A.inv_n_g = 1.0 / s->n_g;
-    A.cert_tol = g_cert_tol;
-    A.cert_tol32 = std::max(g_cert_tol32, g_cert_tol);   // raising the double bound raises this one too
-    A.timeline = g_timeline;
-    A.timeline_waves = g_timeline_waves;
+    A.cert_tol = (dbg && dbg->cert_tol > 0.0) ? dbg->cert_tol : kCertTol;
+    // raising the double bound raises this one too
+    A.cert_tol32 = std::max((dbg && dbg->cert_tol32 > 0.0) ? dbg->cert_tol32 : kCertTol32, A.cert_tol);
+    A.timeline = timeline ? dbg->timeline : nullptr;
+    A.timeline_waves = timeline ? dbg->timeline_waves : 0;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
     A.n_iter = 1;
@@ -1068,7 +1128,9 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         HIP_TRY(hipGetLastError());
         return WGRT_OK;
     }
-    int64_t grid = workgroups > 0 ? workgroups : s->jones_grid[variant == 9][num_iter > 1][single];
+    int64_t grid = c.workgroups > 0 ? c.workgroups
+                   : timeline     ? s->jones_tl_grid[num_iter > 1]
+                                  : s->jones_grid[variant == 9][num_iter > 1][single];
     const int64_t useful = (n_rays + 255) / 256;
     if (grid > useful) grid = useful;
     wgrt_scene *ms = const_cast<wgrt_scene *>(s);
@@ -1084,6 +1146,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         A.n_iter = num_iter;
         A.rng64 = sc->rng64;
         A.iter_epoch = epoch;
+        A.handoff_wait_ticks = (dbg && dbg->handoff_wait_ticks) ? dbg->handoff_wait_ticks
+                                                                : kHandoffTicksPerIter * (unsigned long long)(num_iter + 1);
     }
     A.replay_count = ctr + kHeads * kHeadStride;
     A.replay_list = sc->list;
@@ -1097,7 +1161,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.part = sc->part;
     A.n_trace_waves = (int)grid;   // one partial slot per trace workgroup
     // chunk_order is given in 64-ray chunks; a staged chunk is one ray per lane
-    const int jchunk = A.order ? kChunk : std::min(g_jchunk, 64);
+    const int jchunk = A.order ? kChunk : ((dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk);
     const dim3 g3((unsigned)grid), b3(256);
     // instantiations: cell word width x fused chain x single-wavelength guard
 #define WGRT_LAUNCH_JONES(CELL, LOCV)                                                                              \
@@ -1111,17 +1175,41 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         else                                                                                                       \
             hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false>), g3, b3, 0, st, A, LOCV, ctr, jchunk);\
     } while (0)
-    if (variant == 9) {
+    if (timeline) {
+        const LocatorT<uint32_t> l32 = make_locator32(s);
+        if (num_iter > 1)
+            hipLaunchKernelGGL((trace_jones_tl_kernel<uint32_t, true, false>), g3, b3, 0, st, A, l32, ctr, jchunk);
+        else
+            hipLaunchKernelGGL((trace_jones_tl_kernel<uint32_t, false, false>), g3, b3, 0, st, A, l32, ctr, jchunk);
+    } else if (variant == 9) {
         WGRT_LAUNCH_JONES(uint64_t, A.loc);
     } else {
         const LocatorT<uint32_t> l32 = make_locator32(s);
         WGRT_LAUNCH_JONES(uint32_t, l32);
     }
 #undef WGRT_LAUNCH_JONES
-    HIP_TRY(hipGetLastError());
-    hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
-    HIP_TRY(hipGetLastError());
+    hipError_t e = hipGetLastError();
+    if (e == hipSuccess && dbg && dbg->fail_after_trace) {
+        mark_dirty(ms, sc);
+        return fail(WGRT_ERR_HIP, "fault injection: failed after the trace kernel (wgrt_debug_opts.fail_after_trace)");
+    }
+    if (e == hipSuccess) {
+        hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
+        e = hipGetLastError();
+    }
+    if (e != hipSuccess) {
+        mark_dirty(ms, sc);
+        return fail(WGRT_ERR_HIP, std::string("trace launch: ") + hipGetErrorString(e));
+    }
     return WGRT_OK;
+}
+
+LaunchCfg cfg_of(int variant, int workgroups, bool single) {
+    LaunchCfg c;
+    c.variant = variant;
+    c.workgroups = workgroups;
+    c.single = single;
+    return c;
 }
 
 }  // namespace
@@ -1146,14 +1234,14 @@ wgrt_status wgrt_trace_fullcolor_ex(const wgrt_scene *s, const wgrt_rays *rays, 
                                     wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream,
                                     int variant, int workgroups) {
     return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
-                        variant, workgroups, false);
+                        cfg_of(variant, workgroups, false));
 }
 
 wgrt_status wgrt_trace_fullcolor(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays,
                                  int64_t gid_offset, uint32_t *rng_states, float *matrix_EB,
                                  wgrt_trace_stats *stats, uint32_t *per_ray_bounces, void *stream) {
-    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, 0, 0,
-                        false);
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
+                        cfg_of(0, 0, false));
 }
 
 wgrt_status wgrt_trace_opts(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
@@ -1161,23 +1249,28 @@ wgrt_status wgrt_trace_opts(const wgrt_scene *s, const wgrt_rays *rays, int64_t 
                             uint32_t *per_ray_bounces, void *stream, const wgrt_launch_opts *opts) {
     if (!opts) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL opts");
     if (opts->kernel != 0 && opts->kernel != 1) return fail(WGRT_ERR_INVALID_ARGUMENT, "kernel must be 0 or 1");
-    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
-                        opts->variant, opts->workgroups, opts->kernel == 1, opts->chunk_order, opts->n_chunk_order,
-                        opts->num_iter);
+    LaunchCfg c = cfg_of(opts->variant, opts->workgroups, opts->kernel == 1);
+    c.chunk_order = opts->chunk_order;
+    c.n_chunk_order = opts->n_chunk_order;
+    c.num_iter = opts->num_iter;
+    c.gid_blocks = opts->gid_blocks;
+    c.gid_block_rays = opts->gid_block_rays;
+    c.dbg = opts->debug;
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, c);
 }
 
 wgrt_status wgrt_trace_single_ex(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
                                  uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
                                  uint32_t *per_ray_bounces, void *stream, int variant, int workgroups) {
     return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
-                        variant, workgroups, true);
+                        cfg_of(variant, workgroups, true));
 }
 
 wgrt_status wgrt_trace_single(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
                               uint32_t *rng_states, float *matrix_EB, wgrt_trace_stats *stats,
                               uint32_t *per_ray_bounces, void *stream) {
-    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, 0, 0,
-                        true);
+    return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream,
+                        cfg_of(0, 0, true));
 }
 
 wgrt_status wgrt_scene_classify(const wgrt_scene *s, const double *xy, int64_t n, uint64_t *out_mask,
@@ -1276,12 +1369,6 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
     return WGRT_OK;
 }
 
-int wgrt_debug_set_host_scene(int on) {
-    const int prev = g_host_scene ? 1 : 0;
-    g_host_scene = on != 0;
-    return prev;
-}
-
 wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int64_t bytes) {
     if (!s || !dst) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / dst");
     const size_t ncells = (size_t)s->loc_host.ncx * s->loc_host.ncy;
@@ -1297,29 +1384,6 @@ wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return WGRT_OK;
-}
-
-int wgrt_debug_set_chunk(int rays) {
-    const int prev = g_jchunk;
-    if (rays > 0) g_jchunk = std::min(rays, 64);
-    return prev;
-}
-
-void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves) {
-    g_timeline = n_waves > 0 ? buf : nullptr;
-    g_timeline_waves = n_waves > 0 ? n_waves : 0;
-}
-
-double wgrt_debug_set_cert_tol32(double cert_tol) {
-    const double prev = g_cert_tol32;
-    if (cert_tol > 0.0) g_cert_tol32 = cert_tol;
-    return prev;
-}
-
-double wgrt_debug_set_cert_tol(double cert_tol) {
-    const double prev = g_cert_tol;
-    if (cert_tol > 0.0) g_cert_tol = cert_tol;
-    return prev;
 }
 
 const char *wgrt_status_string(wgrt_status s) {

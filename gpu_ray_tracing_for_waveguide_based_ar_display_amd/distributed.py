@@ -1,24 +1,40 @@
 """Multi-GPU sharding of the bounce kernel: one process per GPU, FoV x wavelength blocks.
 
 Rays are independent and every ray's random stream is keyed by its GLOBAL index
-(RNG seed ``0x9E3779B9 * (gid + 1)``, MAIN:158; zero-state fix-up, GRTF:28-29), so a
-contiguous, R-aligned range of global ray ids -- a set of whole FoV x wavelength
-blocks (layout ``gid = ((ii * NY + jj) * L + l) * R + r``, MAIN:82-115) -- can be traced
-on any GPU with ``gid_offset`` and gives bit-identical results.  Each shard writes only
-the eyebox slabs ``EB[l, n, m]`` of its own blocks, and eyebox values are integer
-counts, so one sum-reduce of ``matrix_EB`` to rank 0 (RCCL over xGMI on MI355X, gloo in
-the CPU tests) reproduces the single-GPU grid exactly.  That reduce is the only
-collective on the path.
+(RNG seed ``0x9E3779B9 * (gid + 1)``, MAIN:158; zero-state fix-up, GRTF:28-29), so any set
+of whole FoV x wavelength blocks (layout ``gid = ((ii * NY + jj) * L + l) * R + r``,
+MAIN:82-115) can be traced on any GPU and gives bit-identical results, provided each local
+ray knows its global id (``GidMap``).
 
-The tracer is pluggable (``trace_fn(rays, rng, eb, gid_offset, num_iter)``) so the same
-sharding / stepping / reduction code runs with the HIP kernel in production (``bench.py``,
+Assignment.  Ray lifetimes differ by FoV and wavelength, so contiguous block ranges load the
+ranks unevenly (the same effect measured across the dies of one GPU).  The
+default assignment is therefore *interleaved*: block ``b = fov * L + k`` goes to rank
+``(fov + k) mod N`` (``rank_blocks``) -- every N-th FoV, with the wavelength rotating, so each rank
+gets a representative mix of FoVs and wavelengths whatever N and L are; ``contiguous`` remains
+available.
+
+Collective.  Each rank writes only the eyebox slabs ``EB[l, n, m]`` of its own blocks, plus --
+through the compiled-numba flat-offset aliasing of an out-coupling exactly on the eyebox edge
+(GRTF:154-165) -- the first ``SPILL`` floats of the slab after one of its own.
+``collect_eyebox`` gathers exactly those bytes to rank 0 (``gather``: each rank sends
+``nb x (9600 + SPILL)`` floats, 1/N of the grid, over its own xGMI link) and rank 0 assembles the
+grid; ``reduce`` is the plain sum-reduce of the whole grid (50.8 MB at 21x21).  Eyebox values are
+integer counts, so both reproduce the single-GPU grid exactly.  That is the only collective on
+the path.
+
+The tracer is pluggable (``trace_fn(rays, rng, eb, gid, num_iter)``, ``gid`` a ``GidMap``) so the
+same sharding / stepping / collection code runs with the HIP kernel in production (``bench.py``,
 the reference-flow driver) and with the CPU oracle in the multi-process CPU tests.
 """
 from __future__ import annotations
 
-from dataclasses import dataclass
+from dataclasses import dataclass, field
+
+import numpy as np
 
 MAX_TRACES_PER_CALL = 255   # wgrt_launch_opts.num_iter
+EB_SLAB = 80 * 120          # one (wavelength, FoV) slab of matrix_EB (MAIN:37)
+SPILL = 121                 # floats of the next slab an edge out-coupling can alias into (ix <= 120 at iy 80)
 
 
 def block_range(n_blocks: int, world: int, rank: int) -> tuple[int, int]:
@@ -28,27 +44,85 @@ def block_range(n_blocks: int, world: int, rank: int) -> tuple[int, int]:
     return rank * n_blocks // world, (rank + 1) * n_blocks // world
 
 
+def rank_blocks(n_blocks: int, world: int, rank: int, assign: str = "interleaved", n_lambda: int = 1) -> np.ndarray:
+    """Global block ids of ``rank`` (ascending): ``interleaved`` -- block ``fov * n_lambda + k`` to
+    rank ``(fov + k) % world`` -- or ``contiguous`` (block_range)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    if assign == "interleaved":
+        b = np.arange(n_blocks, dtype=np.int64)
+        return b[(b // n_lambda + b % n_lambda) % world == rank]
+    if assign == "contiguous":
+        lo, hi = block_range(n_blocks, world, rank)
+        return np.arange(lo, hi, dtype=np.int64)
+    raise ValueError(f"unknown assignment {assign!r}")
+
+
+@dataclass
+class GidMap:
+    """Global id of local ray i: ``block_gid[i // rays_per_block] + i % rays_per_block``."""
+    block_gid: np.ndarray
+    rays_per_block: int
+
+    @property
+    def offset(self) -> int | None:
+        """The single ``gid_offset`` when the blocks are consecutive, else None."""
+        b, R = self.block_gid, self.rays_per_block
+        if len(b) == 0:
+            return 0
+        return int(b[0]) if np.array_equal(b, b[0] + R * np.arange(len(b))) else None
+
+    def runs(self):
+        """Consecutive stretches: ``(local_ray_lo, local_ray_hi, global_gid_lo)``."""
+        b, R = self.block_gid, self.rays_per_block
+        i = 0
+        while i < len(b):
+            j = i + 1
+            while j < len(b) and b[j] == b[j - 1] + R:
+                j += 1
+            yield i * R, j * R, int(b[i])
+            i = j
+
+
 @dataclass
 class Shard:
     rank: int
     world: int
-    block_lo: int
-    block_hi: int
+    blocks: np.ndarray            # global block ids, ascending
     rays_per_block: int
-
-    @property
-    def gid_offset(self) -> int:
-        return self.block_lo * self.rays_per_block
+    assign: str = "interleaved"
+    _gid: GidMap | None = field(default=None, repr=False)
 
     @property
     def n_rays(self) -> int:
-        return (self.block_hi - self.block_lo) * self.rays_per_block
+        return len(self.blocks) * self.rays_per_block
+
+    @property
+    def gid(self) -> GidMap:
+        if self._gid is None:
+            self._gid = GidMap(self.blocks * self.rays_per_block, self.rays_per_block)
+        return self._gid
+
+    @property
+    def gid_offset(self) -> int | None:
+        return self.gid.offset
 
 
 def make_shard(num_fov_x: int, num_fov_y: int, n_lambda: int, rays_per_fov: int, world: int,
-               rank: int) -> Shard:
-    lo, hi = block_range(num_fov_x * num_fov_y * n_lambda, world, rank)
-    return Shard(rank, world, lo, hi, rays_per_fov)
+               rank: int, assign: str = "interleaved") -> Shard:
+    return Shard(rank, world, rank_blocks(num_fov_x * num_fov_y * n_lambda, world, rank, assign, n_lambda),
+                 rays_per_fov, assign)
+
+
+def slab_ids(blocks, num_fov_x: int, num_fov_y: int, lambdas) -> np.ndarray:
+    """Flat slab index ``(lambda * NY + n) * NX + m`` of matrix_EB for each global block
+    ``((m * NY + n) * L + k) * R`` (MAIN:82-115; lambda = lambdas[k])."""
+    b = np.asarray(blocks, dtype=np.int64)
+    L = len(lambdas)
+    fov, k = np.divmod(b, L)
+    m, n = np.divmod(fov, num_fov_y)
+    lam = np.asarray(lambdas, dtype=np.int64)[k]
+    return (lam * num_fov_y + n) * num_fov_x + m
 
 
 def split_calls(steps: int, per_call: int = 1) -> list[int]:
@@ -64,7 +138,7 @@ def split_calls(steps: int, per_call: int = 1) -> list[int]:
     return out
 
 
-def run_steps(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: int = 1, hook=None) -> list[int]:
+def run_steps(trace_fn, rays, rng, eb, gid: GidMap, steps: int, per_call: int = 1, hook=None) -> list[int]:
     """The reference's loop of chained launches (MAIN:169-177) over one shard: ``steps`` traces
     of every ray, each starting from the RNG states the previous one left, issued as calls of
     at most ``per_call`` traces (``trace_fn(..., num_iter=k)``; a fused call gives the results
@@ -74,16 +148,21 @@ def run_steps(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: in
     for j, k in enumerate(calls):
         if hook is not None:
             hook(j, "start")
-        trace_fn(rays, rng, eb, gid_offset, k)
+        trace_fn(rays, rng, eb, gid, k)
         if hook is not None:
             hook(j, "end")
     return calls
 
 
+def _world(group):
+    import torch.distributed as dist
+    return dist.get_world_size(group) if dist.is_initialized() else 1
+
+
 def reduce_eyebox(eb, group=None, dst: int = 0):
     """Sum-reduce the eyebox grid to ``dst`` (exact: integer counts in float32 < 2**24)."""
     import torch.distributed as dist
-    if dist.is_initialized() and dist.get_world_size(group) > 1:
+    if _world(group) > 1:
         if getattr(eb, "is_cuda", False) and dist.get_backend(group) == "gloo":
             # gloo reduces device tensors only as an all-reduce (the bench's one-GPU rehearsal)
             dist.all_reduce(eb, op=dist.ReduceOp.SUM, group=group)
@@ -92,35 +171,102 @@ def reduce_eyebox(eb, group=None, dst: int = 0):
     return eb
 
 
-def trace_job(shard: Shard, build_rays_fn, trace_fn, new_eb, num_iter: int = 4, per_call: int = 1, group=None):
-    """Run the reference's job (``num_iter`` chained launches, MAIN:169-177) on this rank's
-    shard and reduce the eyebox grid to rank 0.
+class EyeboxGather:
+    """Gather of each rank's own eyebox slabs (+ their spill) to rank 0, and the assembly there.
 
-    build_rays_fn(block_lo, block_hi) -> (rays, rng) for the shard (rng seeded with the
-    global ids); trace_fn(rays, rng, eb, gid_offset, num_iter) performs num_iter chained
-    traces in place; new_eb() -> zeroed eyebox grid (numpy array or torch tensor).
+    ``all_blocks[r]``: global block ids of rank r (every rank knows the whole assignment, so
+    the message sizes and placements need no exchange).  The payload is padded to the largest
+    shard, as the collective needs equal sizes."""
+
+    def __init__(self, all_blocks, num_fov_x: int, num_fov_y: int, lambdas, n_lambda_scene: int, device=None):
+        import torch
+        self.n_slabs = n_lambda_scene * num_fov_y * num_fov_x
+        self.world = len(all_blocks)
+        self.nb = max(len(b) for b in all_blocks)
+        self.slabs, self.spill, self.spill_dst = [], [], []
+        for b in all_blocks:
+            s = slab_ids(b, num_fov_x, num_fov_y, lambdas)
+            own = set(s.tolist())
+            # the spill of slab s lands in s + 1; it must travel unless s + 1 is this rank's own
+            # slab (then it is already in that slab's copy) or past the grid (dropped, as the
+            # kernel's guard drops it)
+            sp = np.array([(v + 1) not in own and v + 1 < self.n_slabs for v in s.tolist()], dtype=bool)
+            self.slabs.append(torch.as_tensor(s, dtype=torch.int64, device=device))
+            self.spill.append(torch.as_tensor(sp, device=device))
+            self.spill_dst.append(torch.as_tensor(s[sp] + 1, dtype=torch.int64, device=device))
+
+    def pack(self, eb, rank: int):
+        import torch
+        flat = eb.reshape(self.n_slabs, EB_SLAB)
+        s = self.slabs[rank]
+        out = torch.zeros((self.nb, EB_SLAB + SPILL), dtype=eb.dtype, device=eb.device)
+        out[:len(s), :EB_SLAB] = flat.index_select(0, s)
+        sp = self.spill[rank]
+        if bool(sp.any()):
+            nxt = torch.clamp(s + 1, max=self.n_slabs - 1)
+            out[:len(s), EB_SLAB:] = flat.index_select(0, nxt)[:, :SPILL] * sp[:, None].to(eb.dtype)
+        return out
+
+    def assemble(self, eb, parts) -> None:
+        """Rank 0: rebuild the whole grid in ``eb`` from every rank's packed payload."""
+        flat = eb.reshape(self.n_slabs, EB_SLAB)
+        flat.zero_()
+        for r, p in enumerate(parts):
+            s = self.slabs[r]
+            flat.index_copy_(0, s, p[:len(s), :EB_SLAB])
+        for r, p in enumerate(parts):
+            sp = self.spill[r]
+            if len(self.spill_dst[r]):
+                flat[:, :SPILL].index_add_(0, self.spill_dst[r], p[:len(self.slabs[r])][sp][:, EB_SLAB:])
+
+    def __call__(self, eb, group=None, dst: int = 0):
+        import torch
+        import torch.distributed as dist
+        if _world(group) <= 1:
+            return eb
+        rank = dist.get_rank(group)
+        payload = self.pack(eb, rank)
+        on_gloo_dev = getattr(eb, "is_cuda", False) and dist.get_backend(group) == "gloo"
+        if on_gloo_dev:
+            payload = payload.cpu()   # gloo gathers host tensors (the bench's one-GPU rehearsal)
+        parts = [torch.empty_like(payload) for _ in range(self.world)] if rank == dst else None
+        dist.gather(payload, gather_list=parts, dst=dst, group=group)
+        if rank == dst:
+            self.assemble(eb, [p.to(eb.device) for p in parts] if on_gloo_dev else parts)
+        return eb
+
+
+def trace_job(shard: Shard, build_rays_fn, trace_fn, new_eb, num_iter: int = 4, per_call: int = 1, group=None,
+              collect=None):
+    """Run the reference's job (``num_iter`` chained launches, MAIN:169-177) on this rank's
+    shard and collect the eyebox grid on rank 0.
+
+    build_rays_fn(shard) -> (rays, rng) for the shard (rng seeded with the global ids);
+    trace_fn(rays, rng, eb, gid, num_iter) performs num_iter chained traces in place;
+    new_eb() -> zeroed eyebox grid (numpy array or torch tensor); collect(eb, group) ->
+    the collective (default ``reduce_eyebox``; an ``EyeboxGather`` moves 1/N of the bytes).
     Returns (eb, rng): eb holds the full-job grid on rank 0 (this rank's partial elsewhere).
     """
-    rays, rng = build_rays_fn(shard.block_lo, shard.block_hi)
+    rays, rng = build_rays_fn(shard)
     eb = new_eb()
     if shard.n_rays:
-        run_steps(trace_fn, rays, rng, eb, shard.gid_offset, num_iter, per_call)
-    return reduce_eyebox(eb, group), rng
+        run_steps(trace_fn, rays, rng, eb, shard.gid, num_iter, per_call)
+    return (collect or reduce_eyebox)(eb, group), rng
 
 
-def timed_run(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: int, stats, sync=None, hook=None,
-              group=None):
+def timed_run(trace_fn, rays, rng, eb, gid: GidMap, steps: int, per_call: int, stats, sync=None, hook=None,
+              group=None, collect=None):
     """bench.py's timed region on one rank: barrier + ``sync()``, ``steps`` chained traces of the
-    shard (``run_steps``), the eyebox reduce to rank 0, ``sync()`` + barrier.  ``stats[0]`` (the
-    device bounce counter, zeroed here) is what the tracer adds to.  Returns ``(elapsed, bounces,
-    bounces_local)``: the wall time MAX over ranks, the bounce total SUM over ranks, this rank's
-    own bounces.  The two small all-reduces run on ``stats``'s device (RCCL on the GPU box, gloo
-    in the CPU tests)."""
+    shard (``run_steps``), the eyebox collective to rank 0 (``collect``, default the reduce),
+    ``sync()`` + barrier.  ``stats[0]`` (the device bounce counter, zeroed here) is what the
+    tracer adds to.  Returns ``(elapsed, bounces, bounces_local)``: the wall time MAX over ranks,
+    the bounce total SUM over ranks, this rank's own bounces.  The two small all-reduces run on
+    ``stats``'s device (RCCL on the GPU box, gloo in the CPU tests)."""
     import time
 
     import torch
     import torch.distributed as dist
-    multi = dist.is_initialized() and dist.get_world_size(group) > 1
+    multi = _world(group) > 1
     sync = sync or (lambda: None)
     stats.zero_()
     if multi:
@@ -128,8 +274,8 @@ def timed_run(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: in
     sync()
     t0 = time.perf_counter()
     if steps and (rng.numel() if hasattr(rng, "numel") else len(rng)):
-        run_steps(trace_fn, rays, rng, eb, gid_offset, steps, per_call, hook)
-    reduce_eyebox(eb, group)
+        run_steps(trace_fn, rays, rng, eb, gid, steps, per_call, hook)
+    (collect or reduce_eyebox)(eb, group)
     sync()
     if multi:
         dist.barrier(group)
@@ -145,12 +291,23 @@ def timed_run(trace_fn, rays, rng, eb, gid_offset: int, steps: int, per_call: in
 
 def hip_tracer(scene, variant: int = 0, stats=None):
     """trace_fn for ``run_steps`` / ``trace_job`` using the HIP kernel (torch device tensors);
-    ``stats`` (int64[4] device tensor) is added to by every call."""
-    from .engine import trace_fullcolor
+    ``stats`` (int64[STATS_LEN] device tensor) is added to by every call.  A shard of several
+    block ranges passes its global ids as ``gid_blocks`` (uploaded once per map)."""
+    import torch
 
-    def fn(rays, rng, eb, gid_offset, num_iter=1):
-        trace_fullcolor(scene, rays, rng, eb, gid_offset=gid_offset, stats=stats, variant=variant,
-                        num_iter=num_iter)
+    from .engine import trace_fullcolor
+    cache = {}
+
+    def fn(rays, rng, eb, gid: GidMap, num_iter=1):
+        off = gid.offset
+        if off is not None:
+            trace_fullcolor(scene, rays, rng, eb, gid_offset=off, stats=stats, variant=variant, num_iter=num_iter)
+            return
+        key = id(gid)
+        if key not in cache:
+            cache[key] = (gid, torch.as_tensor(gid.block_gid, dtype=torch.int64, device=rng.device))
+        trace_fullcolor(scene, rays, rng, eb, stats=stats, variant=variant, num_iter=num_iter,
+                        gid_blocks=cache[key][1], gid_block_rays=gid.rays_per_block)
     return fn
 
 
@@ -159,18 +316,30 @@ def hip_shard_builder(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, devic
     MAIN:59-158 without host arrays): only the eight columns the kernel reads."""
     from .engine import init_rays
 
-    def build(block_lo, block_hi):
-        return init_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks=(block_lo, block_hi),
+    def build(shard: Shard):
+        return init_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_list=shard.blocks,
                          device=device, all_columns=False)
     return build
 
 
-def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_lo, block_hi):
-    """Host SoA columns + seeds of one shard (rays.build_rays restricted to the blocks)."""
+def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks):
+    """Host SoA columns + seeds of the global blocks ``blocks`` laid back to back (rays.build_rays
+    restricted to each run of consecutive blocks)."""
     from .rays import build_rays, rng_seeds
-    rays = build_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks=(block_lo, block_hi))
-    return rays, rng_seeds(rays["x"].shape[0], block_lo * rays_per_fov)
+    parts, seeds = [], []
+    R = rays_per_fov
+    for lo_r, hi_r, g in GidMap(np.asarray(blocks, dtype=np.int64) * R, R).runs():
+        b0 = g // R
+        nb = (hi_r - lo_r) // R
+        parts.append(build_rays(points, num_fov_x, num_fov_y, lambdas, R, blocks=(b0, b0 + nb)))
+        seeds.append(rng_seeds(nb * R, g))
+    if not parts:
+        empty = build_rays(points, num_fov_x, num_fov_y, lambdas, R, blocks=(0, 0))
+        return empty, rng_seeds(0, 0)
+    rays = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
+    return rays, np.concatenate(seeds)
 
 
-__all__ = ["block_range", "Shard", "make_shard", "split_calls", "run_steps", "reduce_eyebox", "trace_job", "timed_run",
-           "hip_tracer", "hip_shard_builder", "shard_rays_host", "MAX_TRACES_PER_CALL"]
+__all__ = ["block_range", "rank_blocks", "GidMap", "Shard", "make_shard", "slab_ids", "split_calls", "run_steps",
+           "reduce_eyebox", "EyeboxGather", "trace_job", "timed_run", "hip_tracer", "hip_shard_builder",
+           "shard_rays_host", "MAX_TRACES_PER_CALL", "EB_SLAB", "SPILL"]

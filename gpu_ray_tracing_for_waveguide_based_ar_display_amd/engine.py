@@ -13,7 +13,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import LaunchOpts, Rays, Scene, TraceStats, WgrtError, check, load
+from ._lib import STATS_LEN, DebugOpts, LaunchOpts, Rays, Scene, TraceStats, WgrtError, check, load
 
 RAY_COLUMNS = ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 READ_COLUMNS = ("x", "y", "m", "n", "lmd_num", "te", "tm", "delta_phase")
@@ -50,23 +50,44 @@ def rays_to_device(rays: dict, device="cuda") -> dict:
 def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                     gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                     per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                    workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1) -> None:
+                    workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1,
+                    gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None) -> None:
     """Asynchronous launch on ``stream`` (default: torch's current stream).
 
     rays: dict of device float32 tensors keyed like the reference columns
     (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
     kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
-    accepted too.  stats: optional int64[4] device tensor that is added to
-    (bounces, bad_rays, eyebox_hits, replayed).  chunk_order: optional int32 device
-    permutation of the 64-ray chunks (``schedule_by_lifetime``); results do not depend on it.
-    num_iter: chained traces of every ray (the reference's ``num_iter`` loop of launches,
-    MAIN:169-177) in one call -- results identical to ``num_iter`` calls; the Jones-vector
-    variants run them in one persistent launch (``wgrt_launch_opts.num_iter``).
+    accepted too.  stats: optional int64[STATS_LEN] device tensor that is added to
+    (bounces, bad_rays, eyebox_hits, replayed, handoff_giveups; ``check_stats`` raises on a
+    hand-off give-up).  chunk_order: optional int32 device permutation of the 64-ray chunks
+    (``schedule_by_lifetime``); results do not depend on it.  num_iter: chained traces of every
+    ray (the reference's ``num_iter`` loop of launches, MAIN:169-177) in one call -- results
+    identical to ``num_iter`` calls; the Jones-vector variants run them in one persistent launch
+    (``wgrt_launch_opts.num_iter``).  gid_blocks / gid_block_rays: global ray ids of a shard made of
+    several block ranges (int64 device tensor, first global id of each local block of
+    ``gid_block_rays`` rays; ``gid_offset`` must then be 0).  debug: ``wgrt_debug_opts`` fields
+    (cert_tol, cert_tol32, chunk_rays, timeline (uint64 device tensor), fail_after_trace,
+    handoff_wait_ticks) -- test / profiling hooks.
     """
     if scene.single_lambda:
         raise ValueError("trace_fullcolor needs a full-colour scene; use trace_single for a single-wavelength one")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=False, chunk_order=chunk_order, num_iter=num_iter)
+           workgroups, single=False, chunk_order=chunk_order, num_iter=num_iter, gid_blocks=gid_blocks,
+           gid_block_rays=gid_block_rays, debug=debug)
+
+
+def new_stats(device) -> torch.Tensor:
+    """A zeroed int64 device tensor laid out as ``wgrt_trace_stats``."""
+    return torch.zeros(STATS_LEN, dtype=torch.int64, device=device)
+
+
+def check_stats(stats: torch.Tensor) -> None:
+    """Raise if a fused launch gave up a hand-off (``wgrt_trace_stats.handoff_giveups``): the
+    eyebox grid and RNG states of that call are then wrong (synchronises on ``stats``)."""
+    g = int(stats[4].item())
+    if g:
+        raise WgrtError(f"{g} fused-launch traces gave up waiting for their ray's previous trace "
+                        "(hand-off failure; results of this call are invalid)")
 
 
 def reserve(scene: Scene, n_rays: int, num_iter: int = 1, stream=None) -> None:
@@ -81,7 +102,8 @@ def reserve(scene: Scene, n_rays: int, num_iter: int = 1, stream=None) -> None:
 def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: torch.Tensor,
                  gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                  per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
-                 workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1) -> None:
+                 workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1,
+                 gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None) -> None:
     """One launch of the single-wavelength kernel (``process_rays_kernel_pro``, GRTF:419-831)
     through ``wgrt_trace_single_ex``: no ``lmd_num`` column (ignored if present),
     matrix_EB [NY, NX, 80, 120], branch guard ener * efficiency > 1e-15.  The scene must be
@@ -89,11 +111,31 @@ def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: 
     if not scene.single_lambda:
         raise ValueError("trace_single needs a single-wavelength scene (Scene.from_geometry(..., wavelength=l))")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single=True, chunk_order=chunk_order, num_iter=num_iter)
+           workgroups, single=True, chunk_order=chunk_order, num_iter=num_iter, gid_blocks=gid_blocks,
+           gid_block_rays=gid_block_rays, debug=debug)
+
+
+def _debug_opts(debug: dict | None):
+    if not debug:
+        return None
+    unknown = set(debug) - {f for f, _ in DebugOpts._fields_} - {"timeline"}
+    if unknown:
+        raise ValueError(f"unknown debug options {sorted(unknown)}")
+    d = DebugOpts()
+    for k, v in debug.items():
+        if k == "timeline":
+            if v is not None:
+                if v.dtype != torch.int64 or not v.is_contiguous() or v.numel() % 8:
+                    raise ValueError("timeline must be a contiguous int64 tensor of 8 words per wave")
+                d.timeline = ctypes.c_void_p(v.data_ptr())
+                d.timeline_waves = v.numel() // 8
+        elif k != "timeline_waves":
+            setattr(d, k, v)
+    return d
 
 
 def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single, chunk_order=None, num_iter=1):
+           workgroups, single, chunk_order=None, num_iter=1, gid_blocks=None, gid_block_rays=0, debug=None):
     device = torch.device("cuda", scene.device)
     x = rays["x"]
     N = x.numel() if n_rays is None else int(n_rays)
@@ -113,7 +155,7 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
     if tuple(matrix_EB.shape) != scene.eb_shape():
         raise ValueError(f"matrix_EB shape {tuple(matrix_EB.shape)} != {scene.eb_shape()}")
     if stats is not None:
-        _as_dev(stats, torch.int64, "stats", device, 4)
+        _as_dev(stats, torch.int64, "stats", device, STATS_LEN)
     if per_ray_bounces is not None:
         if per_ray_bounces.dtype not in (torch.int32, torch.uint32):
             raise TypeError("per_ray_bounces must be uint32 / int32")
@@ -124,9 +166,17 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
     n_chunks = (N + CHUNK - 1) // CHUNK
     if chunk_order is not None:
         _as_dev(chunk_order, torch.int32, "chunk_order", device, n_chunks)
+    if gid_blocks is not None:
+        if gid_block_rays < 1:
+            raise ValueError("gid_blocks needs gid_block_rays >= 1")
+        _as_dev(gid_blocks, torch.int64, "gid_blocks", device, (N + gid_block_rays - 1) // gid_block_rays if N else None)
+    dbg = _debug_opts(debug)
     opts = LaunchOpts(1 if single else 0, int(variant), int(workgroups),
                       ctypes.c_void_p(chunk_order.data_ptr()) if chunk_order is not None else None,
-                      n_chunks if chunk_order is not None else 0, int(num_iter))
+                      n_chunks if chunk_order is not None else 0, int(num_iter),
+                      ctypes.c_void_p(gid_blocks.data_ptr()) if gid_blocks is not None else None,
+                      int(gid_block_rays) if gid_blocks is not None else 0,
+                      ctypes.pointer(dbg) if dbg is not None else None)
     check(load().wgrt_trace_opts(
         scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
         ctypes.c_void_p(matrix_EB.data_ptr()),
@@ -136,16 +186,17 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
         "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
 
 
-def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None, heads: int = 8):
-    """Issue order of the 64-ray chunks for ``chunk_order``: within each of the kernel's per-XCD
-    work-queue segments (chunk positions [c * x / heads, c * (x + 1) / heads), include/wgrt.h), the
-    chunks whose rays belong to the (wavelength, FoV) tiles with the longest mean lifetime in a
-    previous launch go first, so the rays that outlive the work queue come from short-lived
-    tiles and the launch's straggler tail shortens; each segment keeps its own chunks (and the
-    tiles they read stay in that XCD's L2).  ``per_ray_bounces`` from an earlier launch of the
-    same batch (``trace_*(per_ray_bounces=...)``), ``tile_of_ray`` any integer tile key per ray
-    (e.g. ``(lmd_num * NX + m) * NY + n``).  Device tensors in, int32 device permutation out (a
-    few small torch ops, no host sync).  A pure scheduling hint: results are unchanged."""
+def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None):
+    """Issue order of the 64-ray chunks for ``chunk_order``: the chunks whose rays belong to the
+    (wavelength, FoV) tiles with the longest mean lifetime in a previous launch go first, so the
+    rays that outlive the work queue come from short-lived tiles.  The kernel's work queue hands
+    out chunk positions in stripes of 16 (stripe s on head s % 8, each head's stripes in
+    increasing order, wgrt_trace.hip), so a global longest-first order is also longest-first on
+    every head.  ``per_ray_bounces`` from an earlier launch of the same batch
+    (``trace_*(per_ray_bounces=...)``), ``tile_of_ray`` any integer tile key per ray (e.g.
+    ``(lmd_num * NX + m) * NY + n``).  Device tensors in, int32 device permutation out (a few
+    small torch ops, no host sync).  A pure scheduling hint: results are unchanged (DESIGN.md
+    §5.4: it measured within noise on C3)."""
     b = per_ray_bounces.to(torch.float32)
     key = tile_of_ray.to(torch.int64)
     nt = int(n_tiles) if n_tiles is not None else int(key.max().item()) + 1
@@ -155,21 +206,32 @@ def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = Non
     N = b.numel()
     first = torch.arange(0, N, CHUNK, device=b.device)
     chunk_key = mean[key[first]]
-    n = chunk_key.numel()
-    seg = torch.arange(n, device=b.device) * heads // n     # segment of each chunk position
-    # sort by (segment asc, lifetime desc): lifetimes are bounded, so one composite key does it
-    comp = seg.to(torch.float64) * 1e9 - chunk_key.to(torch.float64)
-    return torch.argsort(comp, stable=True).to(torch.int32)
+    return torch.argsort(-chunk_key.to(torch.float64), stable=True).to(torch.int32)
+
+
+def block_runs(block_list) -> list[tuple[int, int, int]]:
+    """Runs of consecutive global block ids: ``(local_block_lo, global_block_lo, count)``."""
+    ids = [int(v) for v in block_list]
+    runs, i = [], 0
+    while i < len(ids):
+        j = i + 1
+        while j < len(ids) and ids[j] == ids[j - 1] + 1:
+            j += 1
+        runs.append((i, ids[i], j - i))
+        i = j
+    return runs
 
 
 def init_rays(points, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int, blocks=None,
-              device="cuda", all_columns: bool = True, stream=None):
+              device="cuda", all_columns: bool = True, stream=None, block_list=None):
     """Build a ray batch on the device (``wgrt_rays_init``; replaces MAIN:59-115 and the RNG
     seeding at MAIN:158, bit-identical to ``rays.build_rays`` + ``rays.rng_seeds``).
 
     ``points``: the R/2 origins (numpy or torch float64 [R/2, 2]); ``blocks=(lo, hi)``
-    builds FoV x wavelength blocks [lo, hi) only (one rank's shard, global ids from lo * R).
-    ``all_columns=False`` allocates only the eight columns the kernel reads.
+    builds FoV x wavelength blocks [lo, hi) only (one rank's shard, global ids from lo * R);
+    ``block_list`` (any sequence of global block ids) builds those blocks back to back (an
+    interleaved shard: local block j is global block block_list[j], RNG seeded with its global
+    ids).  ``all_columns=False`` allocates only the eight columns the kernel reads.
     Returns ``(rays, rng_states)``: a dict of float32 tensors and an int32 view of the
     uint32 RNG states."""
     device = torch.device(device)
@@ -178,22 +240,35 @@ def init_rays(points, num_fov_x: int, num_fov_y: int, lambdas, rays_per_fov: int
     R = int(rays_per_fov)
     lam = np.ascontiguousarray(list(lambdas), dtype=np.int32)
     nblk = num_fov_x * num_fov_y * len(lam)
-    lo, hi = (0, nblk) if blocks is None else (int(blocks[0]), int(blocks[1]))
-    if not 0 <= lo <= hi <= nblk:
-        raise ValueError(f"block range {blocks} outside [0, {nblk}]")
+    if block_list is not None:
+        if blocks is not None:
+            raise ValueError("give blocks or block_list, not both")
+        ids = [int(v) for v in block_list]
+        if any(not 0 <= v < nblk for v in ids):
+            raise ValueError(f"block_list has ids outside [0, {nblk})")
+        runs = block_runs(ids)
+        nb = len(ids)
+    else:
+        lo, hi = (0, nblk) if blocks is None else (int(blocks[0]), int(blocks[1]))
+        if not 0 <= lo <= hi <= nblk:
+            raise ValueError(f"block range {blocks} outside [0, {nblk}]")
+        runs, nb = [(0, lo, hi - lo)], hi - lo
     pts = points if isinstance(points, torch.Tensor) else torch.from_numpy(np.asarray(points, dtype=np.float64))
     pts = pts.to(device=device, dtype=torch.float64).contiguous()
     if tuple(pts.shape) != (R // 2, 2):
         raise ValueError(f"points must have shape ({R // 2}, 2), got {tuple(pts.shape)}")
-    N = (hi - lo) * R
+    N = nb * R
     names = RAY_COLUMNS if all_columns else READ_COLUMNS
     rays = {k: torch.empty(N, dtype=torch.float32, device=device) for k in names}
     rng = torch.empty(N, dtype=torch.int32, device=device)
-    cols = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in rays.items()})
-    check(load().wgrt_rays_init(ctypes.c_void_p(pts.data_ptr()), R, int(num_fov_x), int(num_fov_y),
-                                lam.ctypes.data_as(ctypes.c_void_p), len(lam), lo, hi, ctypes.byref(cols),
-                                ctypes.c_void_p(rng.data_ptr()), ctypes.c_void_p(_stream_handle(device, stream))),
-          "wgrt_rays_init")
+    for loc, glo, cnt in runs:
+        off = loc * R * 4   # bytes into every 4-byte column
+        cols = Rays(**{k: ctypes.c_void_p(v.data_ptr() + off) for k, v in rays.items()})
+        check(load().wgrt_rays_init(ctypes.c_void_p(pts.data_ptr()), R, int(num_fov_x), int(num_fov_y),
+                                    lam.ctypes.data_as(ctypes.c_void_p), len(lam), glo, glo + cnt,
+                                    ctypes.byref(cols), ctypes.c_void_p(rng.data_ptr() + off),
+                                    ctypes.c_void_p(_stream_handle(device, stream))),
+              "wgrt_rays_init")
     return rays, rng
 
 
@@ -255,5 +330,6 @@ def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor
     return out
 
 
-__all__ = ["Scene", "WgrtError", "TraceStats", "trace_fullcolor", "trace_single", "init_rays", "schedule_by_lifetime",
+__all__ = ["Scene", "WgrtError", "TraceStats", "STATS_LEN", "new_stats", "check_stats", "block_runs",
+           "trace_fullcolor", "trace_single", "init_rays", "schedule_by_lifetime",
            "rays_to_device", "classify_points", "shadow", "selftest_math", "RAY_COLUMNS", "_lib"]

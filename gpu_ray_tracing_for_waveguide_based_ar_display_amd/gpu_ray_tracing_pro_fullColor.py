@@ -16,8 +16,8 @@ Same flow as the reference script, on the MI355X kernel:
    and ``evaluation(EB / R / num_iter)`` (MAIN:197-198).
 
 Plots and the PNG export (MAIN:199-237) are visual-only and not reproduced.
-Multi-GPU: run under ``torch.distributed.run``; each rank traces a FoV x wavelength block
-range and the eyebox grid is reduced to rank 0 (``distributed.py``).
+Multi-GPU: run under ``torch.distributed.run``; each rank traces an interleaved set of FoV x
+wavelength blocks and the eyebox slabs are gathered to rank 0 (``distributed.py``).
 """
 from __future__ import annotations
 
@@ -44,8 +44,8 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     import torch.distributed as dist
 
     from .couplers_coor import design_geometry
-    from .distributed import hip_shard_builder, hip_tracer, make_shard, reduce_eyebox, run_steps, split_calls
-    from .engine import Scene, reserve
+    from .distributed import EyeboxGather, hip_shard_builder, hip_tracer, make_shard, run_steps, split_calls
+    from .engine import Scene, check_stats, new_stats, reserve
     from .luts import load_luts, synthetic_luts, validate_luts
     from .rays import generate_points_in_polygon
 
@@ -72,9 +72,9 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     shard = make_shard(num_FOV_x, num_FOV_y, len(lambdas), R, world, rank)
     # ray columns and RNG seeds built on the device (MAIN:59-158 without the host arrays:
     # 48 B x N of host memory and its upload at the reference's 100 x 75 x 3 x 5000 default)
-    rays, rng = hip_shard_builder(points, num_FOV_x, num_FOV_y, lambdas, R, dev)(shard.block_lo, shard.block_hi)
+    rays, rng = hip_shard_builder(points, num_FOV_x, num_FOV_y, lambdas, R, dev)(shard)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stats = new_stats(dev)
     num_rays = num_FOV_x * num_FOV_y * len(lambdas) * R
     say(f"Initialization complete: {num_rays:,} rays, {world} GPU(s)\n" + "=" * 60 + "\nSTART GPU RAY TRACING\n" + "=" * 60)
 
@@ -89,11 +89,14 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     t0.record()
     if shard.n_rays:
-        run_steps(hip_tracer(scene, variant, stats), rays, rng, eb, shard.gid_offset, num_iter, per_call)
+        run_steps(hip_tracer(scene, variant, stats), rays, rng, eb, shard.gid, num_iter, per_call)
     t1.record()
     torch.cuda.synchronize()
     kern_s = t0.elapsed_time(t1) / 1e3
-    reduce_eyebox(eb)
+    check_stats(stats)
+    if world > 1:
+        all_blocks = [make_shard(num_FOV_x, num_FOV_y, len(lambdas), R, world, r).blocks for r in range(world)]
+        EyeboxGather(all_blocks, num_FOV_x, num_FOV_y, lambdas, scene.num_lmd, device=dev)(eb)
     if world > 1:
         dist.all_reduce(stats)
     matrix_EB = eb.cpu().numpy()

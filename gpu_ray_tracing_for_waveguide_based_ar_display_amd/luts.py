@@ -60,6 +60,12 @@ PROFILES = {
     "deep": dict(ic=(0.40, 0.05), r0=(0.90, 0.03), r1=(0.03, 0.90),
                  fc_fold=(0.03, 0.10), fc_keep=0.985, fc_back=0.03, fc2_keep=0.955,
                  oc_turn=0.02, oc_out=(0.02, 0.06), oc_keep=0.985),
+    # BASELINE config 5's deep-bounce stress LUT (configs.CONFIGS["C5"], with hops scaled by 0.05):
+    # a better in-coupler (20 % of rays lost there instead of 55 %), 0th-order reflection kept at
+    # 99.5-99.8 %, out-coupling 2-6 % per OC interaction (the default's 6-25 %)
+    "stress": dict(ic=(0.70, 0.10), r0=(0.95, 0.03), r1=(0.03, 0.95),
+                   fc_fold=(0.02, 0.05), fc_keep=0.998, fc_back=0.05, fc2_keep=0.995,
+                   oc_turn=0.03, oc_out=(0.02, 0.06), oc_keep=0.998),
     # Lossless, evenly split interactions: with shortened hops (tests scale lut_gap) rays
     # live for 100+ bounces and ener = prod(e) falls below the single-wavelength kernel's
     # 1e-15 guard (GRTF:444), which the other profiles practically never reach.

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 2
+#define WGRT_ABI_VERSION 3
 
 typedef enum {
     WGRT_OK = 0,
@@ -90,13 +90,16 @@ typedef struct {
 } wgrt_ray_columns;
 
 typedef struct {
-    uint64_t bounces;      /* ray-bounce events: 1 in-coupling + loop iterations, per ray */
-    uint64_t bad_rays;     /* rays skipped for out-of-range m / n / lmd_num; also fused-launch
-                              traces given up after a hand-off wait of 2^24 passes (never in a
-                              correct run: a nonzero count with in-range indices is a bug)     */
-    uint64_t eyebox_hits;  /* rays accumulated into matrix_EB                             */
-    uint64_t replayed;     /* Jones-vector variants: rays abandoned on an uncertain decision and
-                              re-traced with the reference arithmetic (included in the counts above) */
+    uint64_t bounces;          /* ray-bounce events: 1 in-coupling + loop iterations, per ray      */
+    uint64_t bad_rays;         /* rays skipped for out-of-range m / n / lmd_num                    */
+    uint64_t eyebox_hits;      /* rays accumulated into matrix_EB                                  */
+    uint64_t replayed;         /* Jones-vector variants: rays abandoned on an uncertain decision and
+                                  re-traced with the reference arithmetic (included in the counts above) */
+    uint64_t handoff_giveups;  /* fused launches (num_iter > 1): traces given up because the previous
+                                  trace of their ray never handed over within the bound of
+                                  wgrt_launch_opts.num_iter.  Never in a correct
+                                  run: a nonzero count means the eyebox grid and the RNG states of
+                                  this call are wrong, and the Python layer raises on it.           */
 } wgrt_trace_stats;
 
 typedef struct {
@@ -113,6 +116,15 @@ typedef struct {
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon
  * locator) on HIP device `device`.  Replaces MAIN:40-57. */
 wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scene **out);
+
+/* Scene build options (wgrt_scene_create uses the defaults). */
+typedef struct {
+    double cell_mm;   /* locator grid cell (mm); 0 = default 1/128 mm (fastest on C3) */
+    int host_build;   /* 1: build the cell words and tiles on the host (the reference the device build
+                         is checked against; slow); 0: on the device                              */
+} wgrt_scene_opts;
+wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const wgrt_scene_opts *opts,
+                                 wgrt_scene **out);
 wgrt_status wgrt_scene_destroy(wgrt_scene *scene);
 wgrt_status wgrt_scene_get_info(const wgrt_scene *scene, wgrt_scene_info *info);
 
@@ -163,15 +175,15 @@ wgrt_status wgrt_trace_single_ex(const wgrt_scene *scene, const wgrt_rays *rays,
                                  int workgroups);
 
 /* Launch options for wgrt_trace_opts. */
+typedef struct wgrt_debug_opts wgrt_debug_opts;   /* include/wgrt_debug.h (test / profiling hooks) */
 typedef struct {
     int kernel;          /* 0 process_rays_kernel_pro_fullColor, 1 process_rays_kernel_pro (single lambda) */
     int variant;         /* as wgrt_trace_fullcolor_ex (0 auto)                                           */
     int workgroups;      /* persistent variants: resident workgroups (0 auto)                             */
     /* Persistent variants: order in which the 64-ray chunks [64 c, 64 c + 64) are handed to
      * the waves -- a DEVICE int32 permutation of 0 .. ceil(n_rays / 64) - 1, or NULL for
-     * ascending order.  Results do not depend on it (rays are independent); issuing the
-     * chunks of long-lived rays first shortens the launch's straggler tail (see
-     * engine.schedule_by_lifetime).  The permutation is not validated on the device. */
+     * ascending order.  Results do not depend on it (rays are independent).  The permutation
+     * is not validated on the device. */
     const int32_t *chunk_order;
     int64_t n_chunk_order;
     /* Chained traces per call (0 or 1: one).  num_iter = K gives exactly the results of K
@@ -183,6 +195,15 @@ typedef struct {
      * the others issue K launches.  1 <= num_iter <= 255; num_iter > 1 needs
      * per_ray_bounces == NULL and chunk_order == NULL. */
     int num_iter;
+    /* Global ray ids of a shard made of several FoV x wavelength block ranges (multi-GPU
+     * interleaved sharding): when gid_blocks (DEVICE int64[ceil(n_rays / gid_block_rays)]) is
+     * non-NULL, local ray i has global id gid_blocks[i / gid_block_rays] + i % gid_block_rays
+     * and the call's gid_offset must be 0; NULL: global id gid_offset + i.  The global id seeds
+     * the zero-state RNG fix-up (GRTF:28-29) and nothing else, so results equal a single trace
+     * of the whole batch whatever the assignment. */
+    const int64_t *gid_blocks;
+    int64_t gid_block_rays;
+    const wgrt_debug_opts *debug;   /* NULL in production (include/wgrt_debug.h) */
 } wgrt_launch_opts;
 
 /* One launch of either bounce kernel with launch options (everything else as
@@ -226,63 +247,8 @@ wgrt_status wgrt_scene_classify(const wgrt_scene *scene, const double *xy, int64
 wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_mm, const double *xy, int64_t n,
                                        uint64_t *out_mask);
 
-/* Test hook: base of the Jones-vector variants' decision certification bound (default 1e-10;
- * larger values make more decisions uncertain and send more rays through the replay kernel,
- * results unchanged).  Process-wide; returns the previous value (a value <= 0 only queries). */
-double wgrt_debug_set_cert_tol(double cert_tol);
-/* Test hook: base of the single-precision estimate's bound (default 8e-6; the effective value is
- * max(this, cert_tol)).  Larger values send more decisions through the double-precision
- * re-evaluation (results unchanged).  Process-wide; returns the previous value (<= 0 queries). */
-double wgrt_debug_set_cert_tol32(double cert_tol);
-
-/* Certification shadow of the Jones-vector variants (diagnostic; wgrt_shadow.hip).  Traces rays
- * [0, n_rays) with the reference's own arithmetic (unwrapped delta_phase, hypot / atan2 / wrap,
- * GRTF:132-152 and 905-1246) and, at every Monte-Carlo decision, evaluates the Jones-vector lane's
- * thresholds and certification bound tol on the same state.  rng_states (DEVICE, in/out) and the
- * optional per_ray_bounces follow the reference's path, so they equal one launch of the exact
- * kernel; matrix_EB is not written.  stats: DEVICE pointer, ADDED to (zero it yourself); max
- * fields are max-combined.  single: the single-wavelength kernel (threshold 1e-15). */
-typedef struct {
-    uint64_t decisions;          /* Monte-Carlo decisions evaluated                                 */
-    uint64_t uncertain;          /* decisions the Jones lane cannot certify (its rays are replayed)   */
-    uint64_t silent_flips;       /* certified Jones decisions that differ from the reference's: 0    */
-    uint64_t bounces;            /* ray-bounce events traced                                          */
-    uint64_t fallbacks;          /* decisions the single-precision estimate leaves to the double one  */
-    double max_ratio;            /* max over decisions / thresholds of |c_jones64 - c_ref| / tol64    */
-    double max_ratio32;          /* the same for the single-precision estimate against tol32          */
-    double max_ratio_by_depth[6];   /* max_ratio32 by bounce depth [1,10) [10,30) [30,100) [100,300)
-                                       [300,1000) [1000,inf)                                          */
-    uint64_t decisions_by_depth[6];
-    uint64_t ratio_hist[20];     /* decisions by log10 of their ratio32: bucket b = [1e(b-18),
-                                    1e(b-17)); bucket 0 also holds smaller ratios, 19 larger ones    */
-    double max_ener_ratio;       /* single wavelength: max |ener_jones / ener_ref - 1| / tracked bound */
-} wgrt_shadow_stats;
-
-wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,
-                              int single, uint32_t *rng_states, uint32_t *per_ray_bounces, wgrt_shadow_stats *stats,
-                              void *stream);
-
-/* Debug hook (process-wide): while set, every Jones-vector launch records, per wave w < n_waves
- * of its grid, 8 words into the DEVICE buffer buf[8 w ..]: start, queue-exhausted and end times
- * (s_memrealtime, 100 MHz), passes of the wave loop, lane-passes with a ray in flight, XCD id,
- * and the passes and lane-passes before the queue ran dry.
- * buf = NULL or n_waves = 0 turns it off (the default). */
-void wgrt_debug_set_timeline(unsigned long long *buf, int64_t n_waves);
-
-/* Test hook (process-wide): rays per work-queue item of the Jones-vector variants (default 64,
- * at most 64: an item is staged one ray per lane).  Smaller items make a refill span several
- * items; results unchanged.  Returns the previous value (a value <= 0 only queries). */
-int wgrt_debug_set_chunk(int rays);
-
-/* Debug hook (process-wide): scenes created while set are built entirely on the host (cell
- * words and tiles by the same rules, host code) instead of on the device; returns the previous
- * setting.  The host build is the reference the device build is checked against. */
-int wgrt_debug_set_host_scene(int on);
-
-/* Test hook: copies one of a scene's device structures to host memory dst (bytes must equal its
- * size): which = 0 the locator cell words (uint64, ncx * ncy), 1 the exact lane's tiles,
- * 2 the Jones-vector tiles (doubles, tiles * tile / jtile doubles; wgrt_scene_info). */
-wgrt_status wgrt_debug_scene_copy(const wgrt_scene *scene, int which, void *dst, int64_t bytes);
+/* The test / profiling hooks (certification shadow, scene copies, wave timeline, launch
+ * overrides) are declared in include/wgrt_debug.h. */
 
 /* Device math self-test (test hook): for i < n, out[k * n + i] holds
  * k=0 sqrt(a), 1 a / b, 2 hypot_cr(a, b), 3 atan2(a, b), 4 sin(a), 5 cos(a), 6 wrap(a). */

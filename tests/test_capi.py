@@ -12,8 +12,8 @@ from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
 REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
-def declared_symbols():
-    text = open(os.path.join(REPO, "include", "wgrt.h")).read()
+def declared_symbols(header="wgrt.h"):
+    text = open(os.path.join(REPO, "include", header)).read()
     text = re.sub(r"/\*.*?\*/", "", text, flags=re.S)
     return sorted(set(re.findall(r"\b(wgrt_[a-z0-9_]+)\s*\(", text)))
 
@@ -28,11 +28,27 @@ def lib():
 
 def test_header_declares_the_bound_symbols():
     assert declared_symbols() == sorted(_lib.EXPORTED)
+    assert declared_symbols("wgrt_debug.h") == sorted(_lib.EXPORTED_DEBUG)
 
 
 def test_library_exports_every_declared_symbol(lib):
-    for name in declared_symbols():
+    for name in declared_symbols() + declared_symbols("wgrt_debug.h"):
         assert hasattr(lib, name), name
+
+
+def test_no_process_wide_debug_setters(lib):
+    """The ABI-2 process-wide test setters are gone: every hook is per call (wgrt_debug_opts)."""
+    for name in ("wgrt_debug_set_cert_tol", "wgrt_debug_set_cert_tol32", "wgrt_debug_set_timeline",
+                 "wgrt_debug_set_chunk", "wgrt_debug_set_host_scene"):
+        assert not hasattr(lib, name), name
+
+
+def test_struct_layouts_match_header():
+    """ctypes mirrors of the option / stats structs have the C sizes (x86-64 / gfx950 host ABI)."""
+    assert ctypes.sizeof(_lib.TraceStats) == 5 * 8
+    assert ctypes.sizeof(_lib.LaunchOpts) == 4 * 3 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8
+    assert ctypes.sizeof(_lib.DebugOpts) == 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8
+    assert ctypes.sizeof(_lib.SceneOpts) == 16
 
 
 def test_abi_version_and_status_strings(lib):

@@ -28,9 +28,9 @@ def dev():
     return torch.device("cuda", 0)
 
 
-def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0):
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, rays_to_device, trace_fullcolor,
-                                                                           trace_single)
+def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0, debug=None):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, new_stats, rays_to_device,
+                                                                           trace_fullcolor, trace_single)
     wl = getattr(case, "wavelength", None)
     scene = Scene.from_geometry(case.geom, case.luts, wavelength=wl)
     trace = trace_single if wl is not None else trace_fullcolor
@@ -40,9 +40,9 @@ def _trace_case(case, dev, launches, per_ray=True, variant=0, workgroups=0):
     out = []
     for it in range(launches):
         cnt = torch.zeros(case.N, dtype=torch.int32, device=dev)
-        stats = torch.zeros(4, dtype=torch.int64, device=dev)
+        stats = new_stats(dev)
         trace(scene, rays, rng, eb, per_ray_bounces=cnt if per_ray else None, stats=stats,
-              variant=variant, workgroups=workgroups)
+              variant=variant, workgroups=workgroups, debug=debug)
         torch.cuda.synchronize()
         out.append(dict(bounces=cnt.cpu().numpy().view(np.uint32).copy(), stats=stats.cpu().numpy().copy(),
                         rng=rng.cpu().numpy().view(np.uint32).copy(), eb=eb.cpu().numpy().copy()))
@@ -130,13 +130,8 @@ def test_replay_path_forced(dev, cfg, cert_tol):
     rays are abandoned and re-traced by replay_kernel -- results must still equal the oracle
     bit for bit, and the replay counter must show the branch ran."""
     from oracle import OracleScene
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
     c = _config(**cfg)
-    prev = _lib.load().wgrt_debug_set_cert_tol(cert_tol)
-    try:
-        res = _trace_case(c, dev, 2, variant=7)
-    finally:
-        _lib.load().wgrt_debug_set_cert_tol(prev)
+    res = _trace_case(c, dev, 2, variant=7, debug=dict(cert_tol=cert_tol))
     sc = OracleScene.from_geometry(c.geom, c.luts, wavelength=c.wavelength)
     rng = c.fresh_rng()
     eb = np.zeros(c.eb_shape(), np.float32)
@@ -158,13 +153,8 @@ def test_double_precision_reevaluation_forced(dev, cfg):
     nearly every decision to the double-precision re-evaluation; results must still equal the
     oracle bit for bit, with no extra replays at the default double-precision bound."""
     from oracle import OracleScene
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
     c = _config(**cfg)
-    prev = _lib.load().wgrt_debug_set_cert_tol32(0.5)
-    try:
-        res = _trace_case(c, dev, 2, variant=7)
-    finally:
-        _lib.load().wgrt_debug_set_cert_tol32(prev)
+    res = _trace_case(c, dev, 2, variant=7, debug=dict(cert_tol32=0.5))
     sc = OracleScene.from_geometry(c.geom, c.luts, wavelength=c.wavelength)
     rng = c.fresh_rng()
     eb = np.zeros(c.eb_shape(), np.float32)
@@ -183,18 +173,18 @@ def test_replay_rare_at_default_bound(dev):
     assert int(res[0]["stats"][3]) <= 2
 
 
-def _trace_fused(c, dev, num_iter, variant, wavelength=None, gid_offset=0, workgroups=0):
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, rays_to_device, trace_fullcolor,
-                                                                           trace_single)
+def _trace_fused(c, dev, num_iter, variant, wavelength=None, gid_offset=0, workgroups=0, debug=None):
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, new_stats, rays_to_device,
+                                                                           trace_fullcolor, trace_single)
     wl = getattr(c, "wavelength", wavelength)
     scene = Scene.from_geometry(c.geom, c.luts, wavelength=wl)
     trace = trace_single if wl is not None else trace_fullcolor
     rays = rays_to_device(c.rays, dev)
     rng = torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev)
     eb = torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    stats = new_stats(dev)
     trace(scene, rays, rng, eb, stats=stats, variant=variant, num_iter=num_iter, gid_offset=gid_offset,
-          workgroups=workgroups)
+          workgroups=workgroups, debug=debug)
     torch.cuda.synchronize()
     scene.close()
     return rng.cpu().numpy().view(np.uint32).copy(), eb.cpu().numpy().copy(), stats.cpu().numpy().copy()
@@ -212,6 +202,7 @@ def test_fused_iterations_golden(dev, name, variant):
     np.testing.assert_array_equal(eb, case.eb_expected(4))
     assert int(stats[0]) == int(sum(int(b.sum()) for b in case.f["bounces"]))
     assert int(stats[1]) == 0
+    assert int(stats[4]) == 0   # hand-off give-ups
 
 
 @pytest.mark.parametrize("cfg", [
@@ -226,14 +217,9 @@ def test_fused_iterations_match_oracle(dev, cfg, num_iter, variant, cert_tol):
     many rays are abandoned mid-launch and finished (their remaining iterations too) by the
     replay kernel, while the other rays' later iterations skip them."""
     from oracle import OracleScene
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
     c = _config(**cfg)
-    prev = _lib.load().wgrt_debug_set_cert_tol(cert_tol) if cert_tol else None
-    try:
-        rng_g, eb_g, stats = _trace_fused(c, dev, num_iter, variant, gid_offset=0)
-    finally:
-        if cert_tol:
-            _lib.load().wgrt_debug_set_cert_tol(prev)
+    rng_g, eb_g, stats = _trace_fused(c, dev, num_iter, variant, gid_offset=0,
+                                      debug=dict(cert_tol=cert_tol) if cert_tol else None)
     sc = OracleScene.from_geometry(c.geom, c.luts, wavelength=c.wavelength)
     rng = c.fresh_rng()
     eb = np.zeros(c.eb_shape(), np.float32)
@@ -245,26 +231,22 @@ def test_fused_iterations_match_oracle(dev, cfg, num_iter, variant, cert_tol):
     np.testing.assert_array_equal(eb_g, eb)
     assert int(stats[0]) == total
     assert int(stats[2]) == int(round(float(eb.sum())))
+    assert int(stats[4]) == 0
     if cert_tol:
         assert int(stats[3]) > 0
 
 
 @pytest.mark.parametrize("chunk", [13, 24, 64])
 def test_small_work_items_match_oracle(dev, chunk):
-    """Work items smaller than a wave (wgrt_debug_set_chunk) and a batch that is no multiple of
+    """Work items smaller than a wave (wgrt_debug_opts.chunk_rays) and a batch that is no multiple of
     them: a refill then spans several items and meets short ones, so the staged-column buffers
     are reused while lanes still hold rays from them.  One launch and a fused 3-trace call must
     equal the oracle bit for bit."""
     from oracle import OracleScene
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
     c = _config(5, 4, [0, 1, 2], 100)   # 6000 rays
-    prev = _lib.load().wgrt_debug_set_chunk(chunk)
-    try:
-        # two workgroups (8 waves, 512 lanes) for 6000 rays: every lane is refilled many times
-        single = _trace_case(c, dev, 1, variant=7, workgroups=2)
-        rng_f, eb_f, _ = _trace_fused(c, dev, 3, 7, workgroups=2)
-    finally:
-        _lib.load().wgrt_debug_set_chunk(prev)
+    # two workgroups (8 waves, 512 lanes) for 6000 rays: every lane is refilled many times
+    single = _trace_case(c, dev, 1, variant=7, workgroups=2, debug=dict(chunk_rays=chunk))
+    rng_f, eb_f, _ = _trace_fused(c, dev, 3, 7, workgroups=2, debug=dict(chunk_rays=chunk))
     sc = OracleScene.from_geometry(c.geom, c.luts)
     rng = c.fresh_rng()
     eb = np.zeros(c.eb_shape(), np.float32)
@@ -279,13 +261,119 @@ def test_small_work_items_match_oracle(dev, chunk):
 
 
 def test_fused_iterations_repeat_epochs(dev):
-    """Back-to-back fused calls on one stream reuse the granule scratch (launch epochs)."""
+    """One scene and stream, back-to-back calls: fused calls with different num_iter and a
+    single-trace launch between them, each continuing from the RNG states the previous call left.
+    The fused calls after the first run at launch epochs > 1 on granules whose tags the earlier
+    calls left behind (the stale-tag path every bench and multi-call user hits); every call must
+    equal the oracle's chained launches."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, new_stats, rays_to_device,
+                                                                           trace_fullcolor)
+    from oracle import OracleScene
     c = _config(5, 5, [0, 1, 2], 256)
-    a = _trace_fused(c, dev, 3, 7)
-    for _ in range(3):
-        b = _trace_fused(c, dev, 3, 7)
-        np.testing.assert_array_equal(a[0], b[0])
-        np.testing.assert_array_equal(a[1], b[1])
+    scene = Scene.from_geometry(c.geom, c.luts)
+    rays = rays_to_device(c.rays, dev)
+    rng = torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev)
+    eb = torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev)
+    sc = OracleScene.from_geometry(c.geom, c.luts)
+    o_rng = c.fresh_rng()
+    o_eb = np.zeros(c.eb_shape(), np.float32)
+    for num_iter in (3, 3, 1, 2, 5, 1, 4):
+        stats = new_stats(dev)
+        trace_fullcolor(scene, rays, rng, eb, stats=stats, variant=7, num_iter=num_iter)
+        torch.cuda.synchronize()
+        tot = sum(sc.trace(c.rays, o_rng, o_eb)[0] for _ in range(num_iter))
+        np.testing.assert_array_equal(rng.cpu().numpy().view(np.uint32), o_rng, err_msg=f"num_iter {num_iter}")
+        np.testing.assert_array_equal(eb.cpu().numpy(), o_eb, err_msg=f"num_iter {num_iter}")
+        assert int(stats[0]) == tot and int(stats[4]) == 0
+    scene.close()
+
+
+def test_failed_launch_recovers(dev):
+    """A launch that fails after its trace kernel was enqueued (fault injection: the epilogue never
+    runs, so the counter set the next launch would use is never zeroed) must not corrupt the next
+    launch on the stream: the scratch is reset and the following calls equal the oracle."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, WgrtError, rays_to_device,
+                                                                           trace_fullcolor)
+    from oracle import OracleScene
+    c = _config(5, 5, [0, 1, 2], 256)
+    scene = Scene.from_geometry(c.geom, c.luts)
+    rays = rays_to_device(c.rays, dev)
+    sc = OracleScene.from_geometry(c.geom, c.luts)
+    for num_iter in (1, 3):
+        # a good launch first (so the other counter set is in use), then the failing one
+        trace_fullcolor(scene, rays, torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev),
+                        torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev), num_iter=num_iter)
+        with pytest.raises(WgrtError, match="fault injection"):
+            trace_fullcolor(scene, rays, torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev),
+                            torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev), num_iter=num_iter,
+                            debug=dict(fail_after_trace=1))
+        torch.cuda.synchronize()
+        for _ in range(2):
+            rng = torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev)
+            eb = torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev)
+            trace_fullcolor(scene, rays, rng, eb, num_iter=num_iter)
+            torch.cuda.synchronize()
+            o_rng = c.fresh_rng()
+            o_eb = np.zeros(c.eb_shape(), np.float32)
+            for _ in range(num_iter):
+                sc.trace(c.rays, o_rng, o_eb)
+            np.testing.assert_array_equal(rng.cpu().numpy().view(np.uint32), o_rng)
+            np.testing.assert_array_equal(eb.cpu().numpy(), o_eb)
+    scene.close()
+
+
+def test_handoff_giveup_is_counted_and_raised(dev):
+    """A fused launch whose lanes may not wait at all for a ray's previous trace (hand-off bound of
+    one tick) gives those traces up, counts them in wgrt_trace_stats.handoff_giveups, and
+    engine.check_stats raises -- a broken hand-off is never silent (the driver and bench.py check)."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import WgrtError, check_stats
+    c = _config(5, 4, [0, 1, 2], 100)
+    _rng, _eb, stats = _trace_fused(c, dev, 4, 7, workgroups=2, debug=dict(handoff_wait_ticks=1))
+    assert int(stats[4]) > 0
+    with pytest.raises(WgrtError, match="hand-off"):
+        check_stats(torch.from_numpy(stats))
+    # the default bound gives nothing up
+    _rng, _eb, stats = _trace_fused(c, dev, 4, 7, workgroups=2)
+    assert int(stats[4]) == 0
+    check_stats(torch.from_numpy(stats))
+
+
+@pytest.mark.parametrize("num_iter", [1, 3])
+def test_interleaved_shard_gid_map(dev, num_iter):
+    """A shard of scattered FoV x wavelength blocks (multi-GPU interleaved assignment), traced with
+    its global ids as gid_blocks, equals those blocks of one whole-batch trace -- including the
+    zero-state RNG fix-up (GRTF:28-29), forced here by zeroing some rays' states."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import make_shard
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import init_rays, trace_fullcolor
+    from oracle import OracleScene
+    c = _config(5, 4, [0, 1, 2], 128)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+    pts = generate_points_in_polygon(c.geom.IC, 64, rng=np.random.default_rng(1))
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
+    full = build_rays(pts, 5, 4, [0, 1, 2], 128)
+    o_rng = rng_seeds(full["x"].shape[0])
+    zero = np.arange(5, o_rng.size, 997)
+    o_rng[zero] = 0
+    o_eb = np.zeros(c.eb_shape(), np.float32)
+    sc = OracleScene.from_geometry(c.geom, c.luts)
+    for _ in range(num_iter):
+        sc.trace(full, o_rng, o_eb)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene
+    scene = Scene.from_geometry(c.geom, c.luts)
+    eb = torch.zeros(c.eb_shape(), dtype=torch.float32, device=dev)
+    for r in range(3):
+        shard = make_shard(5, 4, 3, 128, 3, r)
+        assert shard.gid_offset is None
+        rays, rng = init_rays(pts, 5, 4, [0, 1, 2], 128, block_list=shard.blocks, device=dev)
+        gids = (shard.blocks[:, None] * 128 + np.arange(128)[None, :]).reshape(-1)
+        z = np.isin(gids, zero)
+        rng[torch.from_numpy(z).to(dev)] = 0
+        gb = torch.from_numpy(shard.gid.block_gid).to(dev)
+        trace_fullcolor(scene, rays, rng, eb, gid_blocks=gb, gid_block_rays=128, num_iter=num_iter)
+        torch.cuda.synchronize()
+        np.testing.assert_array_equal(rng.cpu().numpy().view(np.uint32), o_rng[gids], err_msg=f"rank {r}")
+    np.testing.assert_array_equal(eb.cpu().numpy(), o_eb)
+    scene.close()
 
 
 def test_reserve_then_fused(dev):
@@ -424,7 +512,8 @@ def test_edge_cases(dev):
     bad["m"][:5] = 99.0
     bad["lmd_num"][5:7] = -1.0
     rng2 = torch.from_numpy(c.fresh_rng().view(np.int32)).to(dev)
-    stats = torch.zeros(4, dtype=torch.int64, device=dev)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import new_stats
+    stats = new_stats(dev)
     trace_fullcolor(scene, bad, rng2, torch.zeros_like(eb), stats=stats)
     torch.cuda.synchronize()
     assert int(stats[1]) == 7

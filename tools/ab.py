@@ -31,7 +31,7 @@ pts = generate_points_in_polygon(g.IC, R // 2, rng=np.random.default_rng(1))
 sc = Scene.from_geometry(g, L)
 rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(0, nx * ny * len(lam))
 eb = torch.zeros(sc.eb_shape(), dtype=torch.float32, device=dev)
-st = torch.zeros(4, dtype=torch.int64, device=dev)
+st = torch.zeros(5, dtype=torch.int64, device=dev)
 nl, nf = int(os.environ["AB_LAUNCHES"]), int(os.environ["AB_FUSED"])
 reserve(sc, rays["x"].numel(), nf)
 order = None

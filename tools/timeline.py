@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Wave timeline of one Jones-vector launch (wgrt_debug_set_timeline): where a launch's time goes.
+"""Wave timeline of one Jones-vector launch (wgrt_debug_opts.timeline): where a launch's time goes.
 
 Runs the bench workload (C3 by default), records per wave: start, queue-exhausted and end
 times, passes and lane-passes, and prints a summary: launch span, when the work queue ran dry,
@@ -62,13 +62,11 @@ def main():
     res = []
     for rep in range(a.reps):
         buf.zero_()
-        L.wgrt_debug_set_timeline(ctypes.c_void_p(buf.data_ptr()), nw)
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
-        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter, **kw)
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter, debug=dict(timeline=buf), **kw)
         e1.record()
         torch.cuda.synchronize()
-        L.wgrt_debug_set_timeline(None, 0)
         t = buf.cpu().numpy().reshape(-1, 8)
         t = t[t[:, 0] > 0]
         start, exh, end, passes, lanes, xcc, p_exh, l_exh = (t[:, k].astype(np.float64) for k in range(8))
