@@ -101,3 +101,49 @@ def test_evaluation_on_traced_eyebox():
     delta_e, U_fov, U_EB, img = E.evaluation(eb)
     assert img.shape == (3, 3, 3, 7, 8)
     assert 0.0 <= U_fov <= 1.0 and 0.0 <= U_EB <= 1.0 and np.isfinite(delta_e)
+
+
+# --- the reference's own evaluation() glue, pinned (tests/golden/gen_golden.py evaluation) --------
+# The fixture holds the outputs of the reference's AR_system_evaluation_functions.evaluation run
+# unmodified (with throwaway colour / cv2 stand-ins routed to this module's restatements of those
+# libraries).  Everything EVAL:45-163 computes itself must therefore agree exactly: the 30-px
+# pupil sampling at (8, 12)-px steps, the FoV flip / transpose, the sensor-matrix weighting, the
+# clip / gamma / HSV normalisation chain, the XYZ scaling, the black masks and the U_fov / U_EB
+# reductions.  Tolerance: exact (the same numpy operations in the same order); the colour-science
+# and OpenCV internals behind the stand-ins stay parity-unpinned.
+EVAL_GOLDEN = np.load(__import__("os").path.join(__import__("os").path.dirname(__file__), "golden",
+                                                  "evaluation_golden.npz"), allow_pickle=False)
+EVAL_NAMES = sorted({k.split("/")[0] for k in EVAL_GOLDEN.files})
+
+
+def _eval_input(name):
+    import hashlib
+    import importlib.util
+    import os
+    spec = importlib.util.spec_from_file_location(
+        "gen_golden", os.path.join(os.path.dirname(__file__), "golden", "gen_golden.py"))
+    gen = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(gen)
+    eb2 = gen.eval_input(name)
+    assert hashlib.sha256(np.ascontiguousarray(eb2).tobytes()).hexdigest() == str(EVAL_GOLDEN[f"{name}/input_sha256"])
+    return eb2
+
+
+@pytest.mark.parametrize("name", EVAL_NAMES)
+def test_evaluation_matches_reference_glue(name):
+    eb2 = _eval_input(name)
+    d, uf, ue, img = E.evaluation(eb2)
+    assert d == float(EVAL_GOLDEN[f"{name}/delta_e"])
+    assert uf == float(EVAL_GOLDEN[f"{name}/U_fov"])
+    assert ue == float(EVAL_GOLDEN[f"{name}/U_EB"])
+    want = EVAL_GOLDEN[f"{name}/output_image"]
+    assert img.shape == want.shape and img.dtype == want.dtype
+    np.testing.assert_array_equal(img, want)
+
+
+def test_evaluation_fixture_covers_both_branches():
+    """The cases reach both sides of EVAL's Y == 0 tests: all-dark positions (U_fov term 0,
+    U_EB 0), fully lit ones, and a mixture."""
+    assert float(EVAL_GOLDEN["dense_3x4/U_EB"]) > 0.9
+    assert 0.0 < float(EVAL_GOLDEN["dense_zero_2x2/U_fov"]) < 1.0
+    assert float(EVAL_GOLDEN["g5x4_rgb/U_fov"]) == 0.0
