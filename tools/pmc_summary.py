@@ -19,7 +19,7 @@ merge = sys.argv[sys.argv.index("--merge") + 1] if "--merge" in sys.argv else No
 if merge:
     args.remove(merge)
 root = args[0]
-res, bpl, kname, line = {}, None, None, None
+res, bpl, kname, line, durs = {}, None, None, None, []
 for d in sorted(glob.glob(os.path.join(root, "p*"))):
     log = open(os.path.join(d, "log.txt")).read().splitlines()
     lines = [l for l in log if l.startswith("{")]
@@ -37,6 +37,11 @@ for d in sorted(glob.glob(os.path.join(root, "p*"))):
             per[row["Counter_Name"]][row["Dispatch_Id"]] += float(row["Counter_Value"])
     for c, v in per.items():
         res[c] = sum(v.values()) / len(v)
+    # the trace kernel's own durations in this pass (kernel trace): the clock estimate's denominator
+    for f in glob.glob(os.path.join(d, "**", "*kernel_trace.csv"), recursive=True):
+        for row in csv.DictReader(open(f)):
+            if kname in row["Kernel_Name"]:
+                durs.append((int(row["End_Timestamp"]) - int(row["Start_Timestamp"])) * 1e-9)
 out = {"kernel": kname, "bounces_per_launch": bpl, "counters_per_dispatch": res}
 g = res.get
 if bpl:
@@ -51,8 +56,11 @@ if g("TCC_HIT_sum") is not None and g("TCC_MISS_sum") is not None:
     out["l2_hit_rate"] = g("TCC_HIT_sum") / max(g("TCC_HIT_sum") + g("TCC_MISS_sum"), 1)
 if g("SQ_ACTIVE_INST_VALU") and g("GRBM_GUI_ACTIVE"):
     out["valu_busy_frac"] = 4 * g("SQ_ACTIVE_INST_VALU") / (g("GRBM_GUI_ACTIVE") / 8 * 1024)
-if g("GRBM_GUI_ACTIVE") and line:
-    out["effective_clock_ghz"] = g("GRBM_GUI_ACTIVE") / 8 / (line["roofline"]["launch_avg_ms"] * 1e-3) / 1e9
+if durs:
+    durs.sort()
+    out["kernel_median_s_profiled"] = durs[len(durs) // 2]
+    if g("GRBM_GUI_ACTIVE"):
+        out["effective_clock_ghz"] = g("GRBM_GUI_ACTIVE") / 8 / out["kernel_median_s_profiled"] / 1e9
 print(json.dumps(out, indent=1))
 if len(args) > 1:
     json.dump(out, open(args[1], "w"), indent=1)
@@ -69,7 +77,7 @@ if merge and line:
              "effective_clock_ghz": round(out.get("effective_clock_ghz", float("nan")), 3),
              "note": "rocprofv3 --pmc passes of the trace kernel on this build (tools/pmc_passes.sh); "
                      "valu_busy_frac = SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs); "
-                     "effective clock = GRBM_GUI_ACTIVE / 8 / launch time (HIP events, includes the epilogue)"}
+                     "effective clock = GRBM_GUI_ACTIVE / 8 / the trace kernel's median duration in the profiled passes"}
     data = {}
     if os.path.exists(merge):
         try:
