@@ -12,9 +12,10 @@ from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import single_wavel
 from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds
 
 GOLDEN = os.path.join(os.path.dirname(os.path.abspath(__file__)), "golden")
-# bounce-kernel cases (geometry_tables.npz holds the geometry function's tables: test_geometry_golden)
+# bounce-kernel cases (geometry_tables.npz holds the geometry function's tables: test_geometry_golden;
+# evaluation_golden.npz the evaluation() outputs: test_evaluation)
 CASES = sorted(os.path.splitext(os.path.basename(p))[0] for p in glob.glob(os.path.join(GOLDEN, "*.npz"))
-               if not os.path.basename(p).startswith("geometry_"))
+               if not os.path.basename(p).startswith(("geometry_", "evaluation_")))
 
 
 def input_digest(geom, luts, tir=None, gap=None) -> str:
