@@ -688,86 +688,6 @@ __device__ __forceinline__ bool lane_load_staged(const TraceArgs &A, const LdsU3
     return lane_init(A, i, L, fx, fy, fm, fn, fl, fte, ftm, d, rs);
 }
 
-// ---------------------------------------------------------------------------------------------
-// LDS tile slots.  Every interaction reads its tile's header (moves, miss-hop phasors, cos of the
-// in-coupling angle, phase growth: 128 B) and its block's line 0 (the estimate's input: 80 B).
-// Read from global memory that is 7-9 vector-memory wave-instructions per interaction, each one
-// queued in the CU's load path (TA / TD) behind the cell-word gathers that miss in the caches.
-// A wave therefore keeps the hot part of the tiles of its two most recent work items in LDS
-// (slot s holds the tile of the item staged into ray-column buffer s): header, then line 0 of
-// every block packed at 80 B, copied by three direct-to-LDS 16-B loads per item.  A lane reads
-// its tile through ds_read when its ray's slot still holds its tile (the slot's tag matches the
-// ray's tile index and the copy has landed), else from global memory -- the same bytes, so the
-// results cannot differ; only where they are read from does.  The taken branch's double-precision
-// matrix stays in global memory (one 64-B read per interaction).
-// ---------------------------------------------------------------------------------------------
-constexpr int kSlotHeader = 128;                  // bytes: the Jones tile's header (kJHeader doubles)
-constexpr int kSlotLine = 80;                     // bytes of a block's line 0 the estimate reads
-constexpr int kSlotBlocks = 29;                   // 3 + 2 nfc + 2 noc for the reference's 7 FC / 6 OC slices
-constexpr int kSlotBytes = kSlotHeader + kSlotLine * kSlotBlocks;   // 2448
-constexpr int kSlotPieces = kSlotBytes / 16;      // 16-B pieces copied per slot (153)
-typedef uint8_t __attribute__((address_space(3))) LdsU8;
-
-// Copy tile `jt` (Jones tile, global) into slot S: piece p = 64 i + lane of load i; pieces 0..7 the
-// header, then 5 per block.  Issued by every lane of the wave (exec-masked beyond the last piece).
-__device__ __forceinline__ void stage_tile(const double *jt, LdsU8 *S, int lane, int nblocks) {
-    const int npieces = 8 + 5 * nblocks;
-#pragma unroll
-    for (int i = 0; i < (kSlotPieces + 63) / 64; ++i) {
-        const int p = 64 * i + lane;
-        if (p < npieces) {
-            const int q = p - 8;
-            const int off = p < 8 ? 16 * p : kSlotHeader + (q / 5) * (8 * kJBlock) + 16 * (q % 5);
-            __builtin_amdgcn_global_load_lds((const void *)((const char *)jt + off),
-                                             (void __attribute__((address_space(3))) *)(S + 1024 * i), 16, 0, 0);
-        }
-    }
-}
-
-// The per-interaction reads of a tile's header and of block `blk`'s line 0, from an LDS slot or
-// from the global tile (identical bytes).
-struct TileLine {
-    double2 cg;        // cos(ic1 angle), phase growth G
-    double2 c01;       // cosA_0, cosA_1
-    float4 fw;         // Wsum, cosA_2 (floats)
-    float4 h0, h1, h2; // Hermitian forms of the three branches
-    double2 mva, mvb;  // moves of branch a / b
-    double2 hop;       // miss-hop phasor of the current region
-};
-
-__device__ __forceinline__ void read_line_lds(TileLine &t, const LdsU8 *S, int blk, int ga, int gb, int hopo) {
-    typedef double __attribute__((ext_vector_type(2))) V2d;
-    typedef float __attribute__((ext_vector_type(4))) V4f;
-    typedef const V2d __attribute__((address_space(3))) *D2;
-    typedef const V4f __attribute__((address_space(3))) *F4;
-    auto d2 = [](V2d v) { return double2{v.x, v.y}; };
-    auto f4 = [](V4f v) { return float4{v.x, v.y, v.z, v.w}; };
-    const LdsU8 *B = S + kSlotHeader + kSlotLine * blk;
-    t.cg = d2(*(D2)(S + 8 * kJCosIc1));
-    t.mva = d2(*(D2)(S + 8 * (kJGap + ga)));
-    t.mvb = d2(*(D2)(S + 8 * (kJGap + gb)));
-    t.hop = d2(*(D2)(S + 8 * (kJHop + hopo)));
-    t.c01 = d2(*(D2)(B));
-    t.fw = f4(*(F4)(B + 16));
-    t.h0 = f4(*(F4)(B + 32));
-    t.h1 = f4(*(F4)(B + 48));
-    t.h2 = f4(*(F4)(B + 64));
-}
-
-__device__ __forceinline__ void read_line_global(TileLine &t, const double *T, int blk, int ga, int gb, int hopo) {
-    const double *B = T + kJHeader + kJBlock * blk;
-    t.cg = *(const double2 *)(T + kJCosIc1);
-    t.mva = *(const double2 *)(T + kJGap + ga);
-    t.mvb = *(const double2 *)(T + kJGap + gb);
-    t.hop = *(const double2 *)(T + kJHop + hopo);
-    t.c01 = *(const double2 *)(B + kJBlockCos);
-    t.fw = *(const float4 *)(B + kJBlockF32);
-    const float4 *H = (const float4 *)(B + kJBlockHerm);
-    t.h0 = H[0];
-    t.h1 = H[1];
-    t.h2 = H[2];
-}
-
 struct JField {
     double er, ei, mr, mi;
 };
@@ -879,28 +799,19 @@ __device__ __forceinline__ double4 block_cw(const double *B) {
 
 // The efficiencies from the single-precision Hermitian forms (the estimate every decision starts
 // with).  cw = {cosA_0, cosA_1, cosA_2, Wsum}.
-__device__ __forceinline__ void estimate32(JDecision &d, const TileLine &t, const JRay &r, bool three, double inv,
-                                           double f01, double inv_n_g, const double4 &cw) {
-    const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
-    const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
-    const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
-    const double q0 = (double)herm_form(t.h0, a, b, cr, ci), q1 = (double)herm_form(t.h1, a, b, cr, ci);
-    double q2 = 0.0;
-    if (three) q2 = (double)herm_form(t.h2, a, b, cr, ci);
-    d.a0 = q0 * cw.x * inv * f01;
-    d.a1 = q1 * cw.y * inv * f01;
-    d.a2 = three ? q2 * cw.z * inv * inv_n_g : 0.0;
-}
-
-// The same from a block's line 0 in global memory (the certification shadow).
 __device__ __forceinline__ void estimate32(JDecision &d, const double *B, const JRay &r, bool three, double inv,
                                            double f01, double inv_n_g, const double4 &cw) {
     const float4 *H = (const float4 *)(B + kJBlockHerm);
-    TileLine t;
-    t.h0 = H[0];
-    t.h1 = H[1];
-    t.h2 = three ? H[2] : float4{0.f, 0.f, 0.f, 0.f};
-    estimate32(d, t, r, three, inv, f01, inv_n_g, cw);
+    const float4 h0 = H[0], h1 = H[1];
+    const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
+    const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
+    const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
+    const double q0 = (double)herm_form(h0, a, b, cr, ci), q1 = (double)herm_form(h1, a, b, cr, ci);
+    double q2 = 0.0;
+    if (three) q2 = (double)herm_form(H[2], a, b, cr, ci);
+    d.a0 = q0 * cw.x * inv * f01;
+    d.a1 = q1 * cw.y * inv * f01;
+    d.a2 = three ? q2 * cw.z * inv * inv_n_g : 0.0;
 }
 
 // The same in double precision, one matrix at a time (the rare re-evaluation of a decision the
@@ -933,7 +844,7 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // are the same values the all-double evaluation gives.
 template <bool SINGLE, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
-                                        bool entry, const LdsU8 *slot = nullptr) {
+                                        bool entry) {
     JRay &r = L.r;
     const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
@@ -944,19 +855,15 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    // the tile header and the block's line 0: from the wave's LDS slot when it holds this ray's tile
-    // (slot != NULL), else from global memory -- the same bytes.  Both branches' moves come with
-    // them: the taken branch's new cell word can then be issued together with its matrix.
-    TileLine tl;
-    const int hopo = r.region == 2 ? 0 : 2;
-    if (slot) read_line_lds(tl, slot, blk, ga, gb, hopo);
-    else read_line_global(tl, T, blk, ga, gb, hopo);
-    const double2 cg = tl.cg;   // cos(ic1 angle), phase growth
-    const double4 cw = double4{tl.c01.x, tl.c01.y, (double)tl.fw.y, (double)tl.fw.x};
-    const double2 mva = tl.mva, mvb = tl.mvb;
+    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
+    const double4 cw = block_cw(B);
+    // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
+    // issued together with its matrix, one memory round trip per interaction less
+    const double2 mva = *(const double2 *)(T + kJGap + ga);
+    const double2 mvb = *(const double2 *)(T + kJGap + gb);
     // the miss hops since the last interaction: delta_phase += 2 lut_TIR each (GRTF:1052, ...)
     if (r.hops) {
-        const double2 hop = tl.hop;
+        const double2 hop = *(const double2 *)(T + kJHop + (r.region == 2 ? 0 : 2));
         for (uint32_t h = 0; h < r.hops; ++h) {
             const double mr = r.mr;
             r.mr = fma(mr, hop.x, -r.mi * hop.y);
@@ -972,7 +879,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
     const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
-    estimate32(d, tl, r, three, inv, f01, A.inv_n_g, cw);
+    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     if (!d.ok) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);

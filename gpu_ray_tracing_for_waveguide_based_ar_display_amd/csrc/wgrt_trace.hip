@@ -164,9 +164,6 @@ constexpr int kFusedRefill = 16;
 #ifndef WGRT_STRIPE
 #define WGRT_STRIPE 16
 #endif
-#ifndef WGRT_LDS_TILES
-#define WGRT_LDS_TILES 1   // 0: every tile read from global memory (A/B builds, tools/ab_build.py)
-#endif
 constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
 
 // How long a fused-launch lane may wait for its ray's previous trace before it gives the trace
@@ -259,18 +256,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     // ranges of at most 64 rays.
     int sb = 0;
     uint32_t sbase = 0, sbase_prev = 0;
-    // this wave's two LDS tile slots (wgrt_device.h stage_tile): slot s holds the tile of the item
-    // staged into column buffer s, tagged with its tile index (wave-uniform), usable once its copy
-    // has landed (ready bit s).  A lane reads its tile from slot lslot when that slot's tag is its
-    // ray's tile, else from global memory.
-    __shared__ __attribute__((aligned(16))) uint8_t tile_slot[4][2][kSlotBytes];
-    LdsU8 *const slots = (LdsU8 *)&tile_slot[threadIdx.x >> 6][0][0];
-    const int nblocks = 3 + 2 * A.nfc + 2 * A.noc;
-    const bool lds_tiles = WGRT_LDS_TILES && nblocks <= kSlotBlocks;
-    uint32_t stag0 = 0xffffffffu, stag1 = 0xffffffffu;
-    uint32_t ready = 0;          // bit s: slot s holds the tile stag_s
-    bool tile_dma = false;       // a slot copy was issued in the previous pass
-    int lslot = -1;              // per lane: the slot of this ray's item
     // start the trace (L.i, L.k) on this lane: active, waiting (previous trace still running) or
     // skipped (bad ray / ray already handed to the replay)
     auto start = [&]() {
@@ -280,7 +265,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         const bool ok = lane_load_staged(A, sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
                                          (int)(in_cur ? oc : L.i - sbase_prev), L.i, L,
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
-        lslot = in_cur ? sb : sb ^ 1;
         waiting = false;
         active = false;
         if (!ok) {
@@ -324,13 +308,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     };
 
     for (;;) {
-        if (tile_dma) {
-            // the slot copy issued last pass: every load since then has been waited for except the
-            // youngest few, so this wait costs (almost) nothing; from here on the slot is readable
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-            ready = (stag0 != 0xffffffffu ? 1u : 0u) | (stag1 != 0xffffffffu ? 2u : 0u);
-            tile_dma = false;
-        }
         if (active) {
             blk = advance(A, loc, L, kind);
             entry = false;
@@ -421,27 +398,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         // the rays taken from every item of this refill start together: one round trip for
         // their columns however many items they came from
-        if (staged) {
-            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
-            if (lds_tiles) {
-                // the new item's tile (its first ray's; wave-uniform) into slot sb: read from the
-                // staged columns, copied by three direct-to-LDS loads that land before the next
-                // pass (rays started this pass read their entry block from global memory)
-                const LdsU32 *S = sbufs + sb * (kStageCols * 64);
-                const int fm = (int)__uint_as_float(S[2 * 64]), fn = (int)__uint_as_float(S[3 * 64]);
-                const int fl = KA(l) ? (int)__uint_as_float(S[4 * 64]) : 0;
-                const bool ok = fm >= 0 && fm < A.nx && fn >= 0 && fn < A.ny && fl >= 0 && fl < A.nl;
-                const uint32_t t0 = ok ? (uint32_t)((fl * A.nx + fm) * A.ny + fn) : 0xffffffffu;
-                ready &= ~(1u << sb);
-                if (sb) stag1 = t0;
-                else stag0 = t0;
-                if (ok) {
-                    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");   // reads of the old slot are done
-                    stage_tile(KA(jtiles) + (size_t)t0 * (size_t)A.jtile_d, slots + sb * kSlotBytes, lane, nblocks);
-                    tile_dma = true;
-                }
-            }
-        }
+        if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
         if (taken) {
             start();
             taken = false;
@@ -453,9 +410,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         bool out = false;
         if (active && blk >= 0) {
-            const uint32_t tg = lslot == 1 ? stag1 : stag0;
-            const bool in_lds = lslot >= 0 && ((ready >> lslot) & 1u) && tg == L.tix;
-            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry, in_lds ? slots + lslot * kSlotBytes : nullptr);
+            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
                 retire();
