@@ -925,46 +925,79 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     return ba ? 4 : 5;
 }
 
-// Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246
-// that need no Monte-Carlo interaction, at most kJMaxHops per call: every iteration then tests
-// a cell word loaded a pass earlier (JLane::pf), and a hop issues the load of the next one.  1 measured
-// best on C3 (2 and 4 slower); a compile-time bound, not a kernarg, straightens the loop (-2 %
-// fused).
-constexpr int kJMaxHops = 1;
+// The EDGE classes a lane's loop iteration consults -- eff_reg1's, the region's slices' up to the
+// first IN one, eff_reg2's in R3 -- replaced by the exact predicate's verdict (IN 1 / OUT 0) through
+// the 128-B band records (in_poly_w).  Rare: 0.34 % of C3 lane-passes meet an EDGE cell.
 template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind, int max_hops = kJMaxHops) {
+__device__ __forceinline__ uint64_t resolve_edges(const Loc &loc, uint64_t w, int region, int first, int count,
+                                                  double x, double y) {
+    auto fix = [&](int k) {
+        if (((w >> (2 * k)) & 3u) == 2u) {
+            const bool in = in_poly_w<true>(loc, (typename Loc::Word)w, k, x, y);
+            w = (w & ~(3ull << (2 * k))) | ((uint64_t)(in ? 1u : 0u) << (2 * k));
+        }
+    };
+    fix(kPolyEff1);
+    if (region >= 2) {
+        for (int sl = 0; sl < count; ++sl) {
+            fix(first + sl);
+            if (((w >> (2 * (first + sl))) & 3u) == 1u) break;
+        }
+        if (region == 3) fix(kPolyEff2);
+    }
+    return w;
+}
+
+// Same contract as advance() for the Jones-vector lane: one loop iteration of GRTF:905-1246 that
+// needs no Monte-Carlo interaction (a miss hop or the R3 -> R4 switch: kTransit), or the next
+// interaction's block index, or kDie.  It tests the cell word loaded a pass earlier (JLane::pf);
+// a miss hop issues the load of the next one.  The outcome is computed as selects from the cell
+// word's class bits -- one straight-line evaluation per lane -- and only lanes whose outcome hinges
+// on an EDGE class take the (rare) exact path first: the earlier nested per-slice tests cost
+// every wave-pass the exec-mask bookkeeping of every slice's exact test (SALU per bounce).
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     JRay &r = L.r;
-    auto c = (typename Loc::Word)L.pf;
-    for (int hops = 0;; ++hops) {
-        if (hops >= max_hops) return kTransit;
-        if (L.bounces > (uint32_t)kMaxLoop) return kDie;
-        ++L.bounces;
-        if (!in_poly_w<true>(loc, c, kPolyEff1, r.x, r.y)) return kDie;
-        const int region = r.region;
-        if (region <= 1) {
-            kind = 0;
-            return 1 + region;
-        }
-        // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
-        const bool fc = region <= 3;
-        const int first = fc ? kPolyFC0 : kPolyFC0 + A.nfc, count = fc ? A.nfc : A.noc;
-        const int s = first_slice_w<true>(loc, c, first, count, r.x, r.y);
-        if (s >= 0) {
-            kind = region - 1;
-            return (fc ? 3 + (region - 2) * A.nfc : 3 + 2 * A.nfc + (region - 4) * A.noc) + s;
-        }
-        if (region == 5) return kDie;   // GRTF:1244-1246
-        if (region == 3 && !in_poly_w<true>(loc, c, kPolyEff2, r.x, r.y)) {
-            r.region = 4;   // GRTF:1103-1104: no move, same miss hop (gap[2:4], 2 TIR[1])
-            continue;
-        }
+    uint64_t c = L.pf;
+    const int region = r.region;
+    const int nfc = A.nfc, noc = A.noc;
+    // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
+    const bool fc = region <= 3;
+    const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
+    const uint64_t gmask = count < 32 ? (1ull << (2 * count)) - 1ull : ~0ull;
+    constexpr uint64_t kLow = 0x5555555555555555ull;
+    uint64_t f = (c >> (2 * first)) & gmask;
+    uint64_t in = f & kLow, cand = in | ((f >> 1) & kLow);
+    const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
+    const bool sedge = region >= 2 && cand != 0ull && !((in >> __builtin_ctzll(cand | (1ull << 63))) & 1ull);
+    const bool e2edge = region == 3 && cand == 0ull && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
+    if (e1edge | sedge | e2edge) {
+        c = resolve_edges(loc, c, region, first, count, r.x, r.y);
+        f = (c >> (2 * first)) & gmask;
+        in = f & kLow;
+        cand = in | ((f >> 1) & kLow);
+    }
+    const bool over = L.bounces > (uint32_t)kMaxLoop;   // range(1e5) exhausted (GRTF:905)
+    const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
+    const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
+    const bool ic = region <= 1;
+    const bool hit = !ic & (cand != 0ull);
+    const int sl = __builtin_ctzll(cand | (1ull << 63)) >> 1;
+    const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
+    const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
+    const bool hop = !die & !ic & !hit & !sw;                               // miss hop
+    const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
+    L.bounces += over ? 0u : 1u;
+    kind = ic ? 0 : region - 1;
+    r.region = sw ? 4 : region;
+    if (hop) {
         // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178); its phase step waits for the next interaction
         r.x = r.x + r.gx;
         r.y = r.y + r.gy;
         ++r.hops;
-        c = locate_c(loc, r.x, r.y);   // used from the next pass on (or the next hop of this call)
-        L.pf = c;
+        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
+    return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
 }
 
 template <class LaneT>

@@ -242,8 +242,16 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         int64_t cx = ((ns - x + kHeads - 1) / kHeads) * kStripe;
         if ((ns - 1) % kHeads == x) cx -= kStripe - last;
         if (q >= cx * n_iter) return false;
-        k = (uint32_t)(q / cx);
-        const int64_t r = q % cx;
+        // the item's iteration: 0 for a single trace; else q / cx (< 256) from a double quotient,
+        // corrected -- no 64-bit integer division on the dequeue path
+        int64_t kk = 0;
+        if (FUSED) {
+            kk = (int64_t)((double)q / (double)cx);
+            kk -= kk * cx > q;
+            kk += (kk + 1) * cx <= q;
+        }
+        k = (uint32_t)kk;
+        const int64_t r = q - kk * cx;
         c = ((r / kStripe) * kHeads + x) * kStripe + r % kStripe;
         return true;
     };
