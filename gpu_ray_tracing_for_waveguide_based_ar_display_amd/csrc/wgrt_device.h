@@ -929,12 +929,13 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 // first IN one, eff_reg2's in R3 -- replaced by the exact predicate's verdict (IN 1 / OUT 0) through
 // the 128-B band records (in_poly_w).  Rare: 0.34 % of C3 lane-passes meet an EDGE cell.
 template <class Loc>
-__device__ __forceinline__ uint64_t resolve_edges(const Loc &loc, uint64_t w, int region, int first, int count,
-                                                  double x, double y) {
+__device__ __forceinline__ typename Loc::Word resolve_edges(const Loc &loc, typename Loc::Word w, int region, int first,
+                                                            int count, double x, double y) {
+    using W = typename Loc::Word;
     auto fix = [&](int k) {
         if (((w >> (2 * k)) & 3u) == 2u) {
-            const bool in = in_poly_w<true>(loc, (typename Loc::Word)w, k, x, y);
-            w = (w & ~(3ull << (2 * k))) | ((uint64_t)(in ? 1u : 0u) << (2 * k));
+            const bool in = in_poly_w<true>(loc, w, k, x, y);
+            w = (W)((w & ~((W)3 << (2 * k))) | ((W)(in ? 1u : 0u) << (2 * k)));
         }
     };
     fix(kPolyEff1);
@@ -948,29 +949,37 @@ __device__ __forceinline__ uint64_t resolve_edges(const Loc &loc, uint64_t w, in
     return w;
 }
 
+// lowest set bit of a cell word (undefined for 0: callers guard)
+__device__ __forceinline__ int low_bit(uint32_t v) { return __builtin_ctz(v); }
+__device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); }
+
 // Same contract as advance() for the Jones-vector lane: one loop iteration of GRTF:905-1246 that
 // needs no Monte-Carlo interaction (a miss hop or the R3 -> R4 switch: kTransit), or the next
 // interaction's block index, or kDie.  It tests the cell word loaded a pass earlier (JLane::pf);
 // a miss hop issues the load of the next one.  The outcome is computed as selects from the cell
-// word's class bits -- one straight-line evaluation per lane -- and only lanes whose outcome hinges
-// on an EDGE class take the (rare) exact path first: the earlier nested per-slice tests cost
-// every wave-pass the exec-mask bookkeeping of every slice's exact test (SALU per bounce).
+// word's class bits (in the word's own width: 32 bits for variant 7) -- one straight-line
+// evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
+// exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
+// bookkeeping of every slice's exact test (SALU per bounce).
 template <class Loc>
 __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+    using W = typename Loc::Word;
+    constexpr int kBits = 8 * (int)sizeof(W);
+    constexpr W kLow = (W)0x5555555555555555ull;
+    constexpr W kTop = (W)1 << (kBits - 1);
     JRay &r = L.r;
-    uint64_t c = L.pf;
+    W c = (W)L.pf;
     const int region = r.region;
     const int nfc = A.nfc, noc = A.noc;
     // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
     const bool fc = region <= 3;
     const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
-    const uint64_t gmask = count < 32 ? (1ull << (2 * count)) - 1ull : ~0ull;
-    constexpr uint64_t kLow = 0x5555555555555555ull;
-    uint64_t f = (c >> (2 * first)) & gmask;
-    uint64_t in = f & kLow, cand = in | ((f >> 1) & kLow);
+    const W gmask = 2 * count < kBits ? ((W)1 << (2 * count)) - (W)1 : (W)~(W)0;
+    W f = (c >> (2 * first)) & gmask;
+    W in = f & kLow, cand = in | ((f >> 1) & kLow);
     const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
-    const bool sedge = region >= 2 && cand != 0ull && !((in >> __builtin_ctzll(cand | (1ull << 63))) & 1ull);
-    const bool e2edge = region == 3 && cand == 0ull && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
+    const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
+    const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
     if (e1edge | sedge | e2edge) {
         c = resolve_edges(loc, c, region, first, count, r.x, r.y);
         f = (c >> (2 * first)) & gmask;
@@ -981,8 +990,8 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
     const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
     const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
     const bool ic = region <= 1;
-    const bool hit = !ic & (cand != 0ull);
-    const int sl = __builtin_ctzll(cand | (1ull << 63)) >> 1;
+    const bool hit = !ic & (cand != 0);
+    const int sl = low_bit((W)(cand | kTop)) >> 1;
     const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
     const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
     const bool hop = !die & !ic & !hit & !sw;                               // miss hop

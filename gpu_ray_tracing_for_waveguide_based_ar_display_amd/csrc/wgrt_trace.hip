@@ -179,6 +179,14 @@ constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queu
 // without failing legitimate 1e5-bounce rays.
 constexpr unsigned long long kHandoffTicksPerIter = 100000000ull;   // s_memrealtime: 100 MHz
 
+// A wave-uniform copy of v (lane 0's value, in SGPRs): the wave loop's queue state is uniform,
+// and keeping it scalar lets its branches be scalar branches instead of exec-mask juggling.
+__device__ __forceinline__ unsigned long long uni64(unsigned long long v) {
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)v);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(v >> 32));
+    return ((unsigned long long)hi << 32) | lo;
+}
+
 __device__ __forceinline__ int xcc_id() {
     unsigned v;
     asm volatile("s_getreg_b32 %0, hwreg(HW_REG_XCC_ID)" : "=s"(v));
@@ -363,7 +371,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                     const int x = (head + tries) & (kHeads - 1);
                     unsigned long long q = 0;
                     if (lane == 0) q = atomicAdd(heads + kHeadStride * x, 1ull);
-                    q = __shfl(q, 0);
+                    q = uni64(__shfl(q, 0));
                     if (decode(x, (int64_t)q, c, k)) {
                         head = x;
                         got = true;
@@ -446,7 +454,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             unsigned long long nb = 0;
             if (nout > rem) {
                 if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
-                nb = __shfl(nb, 0);
+                nb = uni64(__shfl(nb, 0));
             }
             if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
                 const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
