@@ -617,44 +617,19 @@ constexpr double kCertTol32 = 8e-6;
 // so the decision is straight-line code instead of nested divergent branches.
 #pragma clang diagnostic ignored "-Wbitwise-instead-of-logical"
 
-// Every column load is issued before anything branches on a loaded value, so a refill waits
-// for one memory round trip (not one for the FoV / wavelength indices and another for the
-// rest).  Fused launches pass the ray's hand-off granule address: it is loaded with the columns.
-__device__ __forceinline__ bool lane_init(const TraceArgs &A, int64_t i, JLane &L, float fx, float fy, float fm,
-                                          float fn, float fl, float fte, float ftm, float d, uint32_t rs) {
-    const int m = (int)fm, n = (int)fn, l = (int)fl;
-    const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
-    L.i = (uint32_t)i;
-    L.tix = ok ? (uint32_t)((l * A.nx + m) * A.ny + n) : 0u;
-    L.r.x = (double)fx;
-    L.r.y = (double)fy;
-    const double te = (double)fte, tm = (double)ftm;
-    double sd = 0.0, cd = 1.0;
-    if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
-    // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
-    L.r.er = te;
-    L.r.ei = 0.0;
-    L.r.mr = cd * tm;
-    L.r.mi = sd * tm;
-    L.r.cos_t = 1.0;
-    L.r.ener = 1.0;
-    L.r.eerr = 0.0;
-    L.r.gx = L.r.gy = 0.0;
-    L.r.hops = 0;
-    L.r.s = rs;
-    L.r.region = 0;
-    L.bounces = 1;
-    L.pf = 0ull;
-    return ok;
-}
-
 // Ray columns staged in LDS a work-queue chunk at a time: the wave that dequeues a chunk of
 // at most 64 rays copies their nine columns (wgrt_rays order below; lmd_num 0 when absent)
 // into its LDS buffer with one direct-to-LDS load per column (lane j <- ray base + j: no
-// VGPR destinations, every lane of the wave busy), and the lanes it refills from that chunk
-// later read their ray from there.  A refill then costs LDS reads instead of nine per-lane
-// gathers and a memory round trip, except right after a dequeue.
+// VGPR destinations, every lane of the wave busy); once they have landed, lane j turns slot j
+// into the ray's start state (prep_staged), and the lanes it refills from that chunk later
+// read their ray from there.  A refill then costs LDS reads instead of nine per-lane gathers,
+// a memory round trip and the start phase's sincos (a refill runs in almost every bulk pass:
+// the sincos on the refilled lanes alone was ~15 % of a pass's instructions; per chunk, all
+// 64 lanes compute it once).
 constexpr int kStageCols = 9;   // x, y, m, n, lmd_num, te, tm, delta_phase, rng
+// ... and the prepared slot: x, y, tile index (kBadTix: FoV / wavelength index out of range),
+// Etm's real part (lo, hi), te, Etm's imaginary part (lo, hi), rng
+constexpr uint32_t kBadTix = 0xffffffffu;
 typedef uint32_t __attribute__((address_space(3))) LdsU32;
 
 __device__ __forceinline__ void glds4(const void *g, LdsU32 *dst) {
@@ -675,17 +650,50 @@ __device__ __forceinline__ void stage_chunk(const TraceArgs &A, LdsU32 *S, int64
     glds4(KA(rng) + ray, S + 8 * 64);
 }
 
-// lane_load from a staged chunk: slot j of buffer S (the loads that filled it have landed).
-__device__ __forceinline__ bool lane_load_staged(const TraceArgs &A, const LdsU32 *S, int j, int64_t i, JLane &L,
+// Slot j of a staged chunk (its loads have landed) -> the ray's start state, in place: lane j
+// of the wave that dequeued the chunk, for every ray of it at once.
+__device__ __forceinline__ void prep_staged(const TraceArgs &A, LdsU32 *S, int j) {
+    const int m = (int)__uint_as_float(S[2 * 64 + j]), n = (int)__uint_as_float(S[3 * 64 + j]);
+    const int l = KA(l) ? (int)__uint_as_float(S[4 * 64 + j]) : 0;
+    const float ftm = __uint_as_float(S[6 * 64 + j]), d = __uint_as_float(S[7 * 64 + j]);
+    const bool ok = m >= 0 && m < A.nx && n >= 0 && n < A.ny && l >= 0 && l < A.nl;
+    const double tm = (double)ftm;
+    double sd = 0.0, cd = 1.0;
+    if (d != 0.0f) sincos((double)d, &sd, &cd);   // phase = cos + i sin (GRTF:136), exact at 0
+    // te_in = Ete, tm_in = phase * Etm (GRTF:137-138)
+    const double mr = cd * tm, mi = sd * tm;
+    S[2 * 64 + j] = ok ? (uint32_t)((l * A.nx + m) * A.ny + n) : kBadTix;
+    S[3 * 64 + j] = (uint32_t)__double_as_longlong(mr);
+    S[4 * 64 + j] = (uint32_t)((uint64_t)__double_as_longlong(mr) >> 32);
+    S[6 * 64 + j] = (uint32_t)__double_as_longlong(mi);
+    S[7 * 64 + j] = (uint32_t)((uint64_t)__double_as_longlong(mi) >> 32);
+}
+
+// A lane's ray from slot j of a prepared chunk.  Fused launches pass the ray's hand-off granule
+// address: it is loaded with the slot.  False: a bad ray (not traced).
+__device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t i, JLane &L,
                                                  const uint64_t *granule = nullptr, uint64_t *gword = nullptr) {
-    const float fx = __uint_as_float(S[0 * 64 + j]), fy = __uint_as_float(S[1 * 64 + j]);
-    const float fm = __uint_as_float(S[2 * 64 + j]), fn = __uint_as_float(S[3 * 64 + j]);
-    const float fl = KA(l) ? __uint_as_float(S[4 * 64 + j]) : 0.0f;
-    const float fte = __uint_as_float(S[5 * 64 + j]), ftm = __uint_as_float(S[6 * 64 + j]);
-    const float d = __uint_as_float(S[7 * 64 + j]);
-    const uint32_t rs = S[8 * 64 + j];
+    const uint32_t tix = S[2 * 64 + j];
+    L.i = (uint32_t)i;
+    L.tix = tix == kBadTix ? 0u : tix;
+    L.r.x = (double)__uint_as_float(S[0 * 64 + j]);
+    L.r.y = (double)__uint_as_float(S[1 * 64 + j]);
+    L.r.er = (double)__uint_as_float(S[5 * 64 + j]);
+    L.r.ei = 0.0;
+    L.r.mr = __longlong_as_double((long long)(((uint64_t)S[4 * 64 + j] << 32) | S[3 * 64 + j]));
+    L.r.mi = __longlong_as_double((long long)(((uint64_t)S[7 * 64 + j] << 32) | S[6 * 64 + j]));
+    L.r.s = S[8 * 64 + j];
     if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    return lane_init(A, i, L, fx, fy, fm, fn, fl, fte, ftm, d, rs);
+    L.r.cos_t = 1.0;
+    L.r.ener = 1.0;
+    L.r.eerr = 0.0;
+    L.r.gx = L.r.gy = 0.0;
+    L.r.hops = 0;
+    L.r.region = 0;
+    L.bounces = 1;
+    // L.pf is not set: the first pass runs the in-coupling interaction, which loads it (and a
+    // write here would wait for the cell loads other lanes' miss hops have in flight)
+    return tix != kBadTix;
 }
 
 struct JField {

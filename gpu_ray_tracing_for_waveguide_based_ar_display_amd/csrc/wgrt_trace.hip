@@ -161,6 +161,7 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
 // spread over 8 addresses; a wave whose head runs dry moves on to the next head.  The XCD id
 // steers placement only: any wave may take any chunk, so correctness never depends on it.
 constexpr int kFusedRefill = 16;
+
 #ifndef WGRT_STRIPE
 #define WGRT_STRIPE 16
 #endif
@@ -278,7 +279,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         uint64_t w = 0;
         const uint32_t oc = L.i - sbase;
         const bool in_cur = oc < 64u;
-        const bool ok = lane_load_staged(A, sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
+        const bool ok = lane_load_staged(sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
                                          (int)(in_cur ? oc : L.i - sbase_prev), L.i, L,
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
         waiting = false;
@@ -321,6 +322,60 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             if (!FUSED && pr) pr[L.i] = L.bounces;
         }
         active = false;
+    };
+
+    // the second half of a pass: the interaction of the lanes at one, then this pass's
+    // out-couplings into the wave's block of queue slots (a contended returning atomic per pass
+    // would put its latency on every pass; a new block is needed about once per hundred passes)
+    auto interact_pass = [&]() {
+        if (TL && tl_on) {
+            ++tl_passes;
+            tl_lanes += __popcll(__ballot(active));
+        }
+        bool out = false;
+        if (active && blk >= 0) {
+            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
+            if (next == kOut) {
+                out = true;
+                retire();
+            } else if (next == kUncertain) {
+                // abandoned with no side effect; replay_kernel re-traces it (fused: from this
+                // iteration on, so later iterations skip the ray)
+                if (FUSED)
+                    __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+                active = false;
+            } else if (next < 0) {
+                retire();
+            } else {
+                L.r.region = next;
+            }
+        }
+        const uint64_t om = __ballot(out);
+        if (om != 0ull) {
+            const int nout = __popcll(om), rem = kQBlock - qfill;
+            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0));
+            unsigned long long nb = 0;
+            if (nout > rem) {
+                if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
+                nb = uni64(__shfl(nb, 0));
+            }
+            if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
+                const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
+                KA(q_xy)[j] = double2{L.r.x, L.r.y};
+                KA(q_i)[j] = L.tix;
+            }
+            if (nout > rem) {
+                // the old block is full: the epilogue bins it
+                if (qblk && lane == 0) KA(full_list)[atomicAdd(KA(full_count), 1ull)] = (uint32_t)(qbase / kQBlock);
+                qbase = nb;
+                qfill = nout - rem;
+                qblk = true;
+            } else {
+                qfill += nout;
+            }
+        }
     };
 
     for (;;) {
@@ -414,62 +469,38 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         // the rays taken from every item of this refill start together: one round trip for
         // their columns however many items they came from
-        if (staged) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
+        if (staged) {
+            asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
+            // lane j prepares slot j of the new chunk; the LDS stores precede the refilled lanes'
+            // reads of other lanes' slots in the wave's (in-order) LDS queue
+            if (lane < (int)(end - (int64_t)sbase)) prep_staged(A, sbufs + sb * (kStageCols * 64), lane);
+            asm volatile("" ::: "memory");
+        }
         if (taken) {
             start();
             taken = false;
         }
         if (__ballot(active || waiting) == 0ull) break;   // queue exhausted, nothing in flight
-        if (TL && tl_on) {
-            ++tl_passes;
-            tl_lanes += __popcll(__ballot(active));
-        }
-        bool out = false;
-        if (active && blk >= 0) {
-            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
-            if (next == kOut) {
-                out = true;
-                retire();
-            } else if (next == kUncertain) {
-                // abandoned with no side effect; replay_kernel re-traces it (fused: from this
-                // iteration on, so later iterations skip the ray)
-                if (FUSED)
-                    __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
-                active = false;
-            } else if (next < 0) {
-                retire();
-            } else {
-                L.r.region = next;
+        // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
+        // the tail loop below
+        if (!FUSED && exhausted) break;
+        interact_pass();
+    }
+    if (!FUSED && __ballot(active) != 0ull) {
+        // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
+        // flight when the queue ran dry finish without the refill's code and ballots on every pass
+        // (-1.6 % per single launch on C3).  Issuing both branches' matrices or both candidate
+        // cell words before the decision here (one or two round trips less per interaction) lost
+        // 1.5 % and 6 %: the chip is still full of rays when the queue runs dry.
+        // The first pass continues the one the main loop broke off (advance and refill done).
+        for (bool first = true;; first = false) {
+            if (!first && active) {
+                blk = advance(A, loc, L, kind);
+                entry = false;
+                if (blk == kDie) retire();
             }
-        }
-        // out-couplings of this pass go to the wave's block of queue slots (a contended returning
-        // atomic per pass would put its latency on every pass; a new block is needed about
-        // once per hundred passes)
-        const uint64_t om = __ballot(out);
-        if (om != 0ull) {
-            const int nout = __popcll(om), rem = kQBlock - qfill;
-            const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0));
-            unsigned long long nb = 0;
-            if (nout > rem) {
-                if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
-                nb = uni64(__shfl(nb, 0));
-            }
-            if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
-                const unsigned long long j = rank < rem ? qbase + qfill + rank : nb + (rank - rem);
-                KA(q_xy)[j] = double2{L.r.x, L.r.y};
-                KA(q_i)[j] = L.tix;
-            }
-            if (nout > rem) {
-                // the old block is full: the epilogue bins it
-                if (qblk && lane == 0) KA(full_list)[atomicAdd(KA(full_count), 1ull)] = (uint32_t)(qbase / kQBlock);
-                qbase = nb;
-                qfill = nout - rem;
-                qblk = true;
-            } else {
-                qfill += nout;
-            }
+            if (__ballot(active) == 0ull) break;
+            interact_pass();
         }
     }
     // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one

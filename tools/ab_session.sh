@@ -1,6 +1,6 @@
 #!/bin/bash
 # One A/B GPU session: parity tests of the tree's library, then tools/ab.py over exp_libs builds and
-# one instruction-count PMC pass of the tree's library.   NAMES="base adv"  TAG=r03d  TESTS=...
+# one instruction-count PMC pass of the tree's library.   NAMES="base adv"  TAG=r03d  TESTS=...  PARITY="adv"
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out
 TAG=${TAG:-ab}
@@ -9,6 +9,13 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 --timeout-method thread > "$OUT/${TAG}_pytest.log" 2>&1
 rc=$?; echo "pytest rc $rc"; tail -3 "$OUT/${TAG}_pytest.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
+# PARITY="name ...": the same tests on exp_libs builds (WGRT_LIB)
+for v in $PARITY; do
+  WGRT_LIB=$(pwd)/exp_libs/$v/libwgrt.so timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 \
+    --timeout-method thread > "$OUT/${TAG}_pytest_$v.log" 2>&1
+  rc=$?; echo "pytest $v rc $rc"; tail -2 "$OUT/${TAG}_pytest_$v.log"
+  if [ $rc -ne 0 ]; then exit $rc; fi
+done
 timeout -k 10 400 python tools/ab.py ${NAMES:-base adv} --rounds ${ROUNDS:-4} --config C3 > "$OUT/${TAG}_ab_C3.log" 2>&1 || exit $?
 grep SUMMARY "$OUT/${TAG}_ab_C3.log"
 if [ -n "$C5" ]; then

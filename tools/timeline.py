@@ -30,26 +30,19 @@ def main():
                     help="chunk issue order: ascending, or long-lived tiles first (from a previous launch)")
     a = ap.parse_args()
     import torch
-    import bench
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd import _lib
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS, build_inputs
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder, make_shard
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, schedule_by_lifetime, trace_fullcolor
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
 
     dev = torch.device("cuda", 0)
-    cfg = bench.CONFIGS[a.config]
-    nx, ny, lam, R = cfg["nx"], cfg["ny"], list(cfg["lambdas"]), cfg["R"]
-    geom = design_geometry(nx, ny)
-    luts = synthetic_luts(geom, seed=0, profile=cfg["profile"])
-    pts = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
+    w = CONFIGS[a.config]
+    nx, ny, lam, R = w.nx, w.ny, list(w.lambdas), w.R
+    geom, luts, pts = build_inputs(w)
     scene = Scene.from_geometry(geom, luts)
-    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(0, nx * ny * len(lam))
+    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(make_shard(nx, ny, len(lam), R, 1, 0))
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     nw = 256 * 8 * 4 * 2
     buf = torch.zeros(8 * nw, dtype=torch.int64, device=dev)
-    L = _lib.load()
     order = None
     if a.order == "lifetime":
         per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
@@ -95,7 +88,6 @@ def main():
             np.savez_compressed(f"{a.raw}.{rep}.npz", start=start, exh=exh, end=end, passes=passes, lanes=lanes,
                                 xcc=xcc, p_exh=p_exh, l_exh=l_exh)
         r["order"] = a.order
-        r["drain_hops"] = int(os.environ.get("WGRT_DRAIN_HOPS", "1"))
         res.append(r)
         print(json.dumps(r), flush=True)
     if a.out:
