@@ -13,6 +13,13 @@ default assignment is therefore *interleaved*: block ``b = fov * L + k`` goes to
 gets a representative mix of FoVs and wavelengths whatever N and L are; ``contiguous`` remains
 available.
 
+Replicas (weak scaling).  ``replica_shard`` gives rank r the WHOLE batch again as replica r: the
+same FoV x wavelength blocks and ray columns, with global ids ``r * N + i`` (N rays per replica),
+so its random streams are its own.  N ranks then trace the reference's kernel over the batch's
+columns tiled N times (RNG seeded by global index, MAIN:158) -- per-GPU work fixed as N grows, the
+shape bench.py measures at N > 1 -- and every rank writes every slab, so the collective is the
+sum-reduce of the grid (the north star's single RCCL reduce of the eyebox over xGMI).
+
 Collective.  Each rank writes only the eyebox slabs ``EB[l, n, m]`` of its own blocks, plus --
 through the compiled-numba flat-offset aliasing of an out-coupling exactly on the eyebox edge
 (GRTF:154-165) -- the first ``SPILL`` floats of the slab after one of its own.
@@ -91,6 +98,7 @@ class Shard:
     blocks: np.ndarray            # global block ids, ascending
     rays_per_block: int
     assign: str = "interleaved"
+    gid_base: int = 0             # global id of the first ray of block 0 (replica r: r * rays of the batch)
     _gid: GidMap | None = field(default=None, repr=False)
 
     @property
@@ -100,7 +108,7 @@ class Shard:
     @property
     def gid(self) -> GidMap:
         if self._gid is None:
-            self._gid = GidMap(self.blocks * self.rays_per_block, self.rays_per_block)
+            self._gid = GidMap(self.gid_base + self.blocks * self.rays_per_block, self.rays_per_block)
         return self._gid
 
     @property
@@ -112,6 +120,33 @@ def make_shard(num_fov_x: int, num_fov_y: int, n_lambda: int, rays_per_fov: int,
                rank: int, assign: str = "interleaved") -> Shard:
     return Shard(rank, world, rank_blocks(num_fov_x * num_fov_y * n_lambda, world, rank, assign, n_lambda),
                  rays_per_fov, assign)
+
+
+def replica_shard(num_fov_x: int, num_fov_y: int, n_lambda: int, rays_per_fov: int, world: int,
+                  rank: int) -> Shard:
+    """Replica ``rank`` of the whole batch (weak scaling): every block, global ids offset by
+    ``rank`` times the batch's ray count."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} / world {world}")
+    nb = num_fov_x * num_fov_y * n_lambda
+    return Shard(rank, world, np.arange(nb, dtype=np.int64), rays_per_fov, "replica",
+                 gid_base=rank * nb * rays_per_fov)
+
+
+def seeds_like(rng, gid: "GidMap"):
+    """RNG seeds ``0x9E3779B9 * (gid + 1)`` (MAIN:158) of a shard's rays, written into ``rng``
+    (a torch int32 view of the uint32 states, or a numpy uint32 array)."""
+    R = gid.rays_per_block
+    if hasattr(rng, "is_cuda"):
+        import torch
+        b = torch.as_tensor(gid.block_gid, dtype=torch.int64, device=rng.device)
+        g = (b[:, None] + torch.arange(R, dtype=torch.int64, device=rng.device)[None, :]).reshape(-1)
+        v = ((g + 1) * 0x9E3779B9) & 0xFFFFFFFF
+        rng.copy_(torch.where(v >= 2 ** 31, v - 2 ** 32, v).to(torch.int32))
+        return rng
+    g = (np.asarray(gid.block_gid, dtype=np.uint64)[:, None] + np.arange(R, dtype=np.uint64)[None, :]).reshape(-1)
+    rng[:] = ((g + np.uint64(1)) * np.uint64(0x9E3779B9) & np.uint64(0xFFFFFFFF)).astype(np.uint32)
+    return rng
 
 
 def slab_ids(blocks, num_fov_x: int, num_fov_y: int, lambdas) -> np.ndarray:
@@ -317,14 +352,18 @@ def hip_shard_builder(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, devic
     from .engine import init_rays
 
     def build(shard: Shard):
-        return init_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_list=shard.blocks,
-                         device=device, all_columns=False)
+        rays, rng = init_rays(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, block_list=shard.blocks,
+                              device=device, all_columns=False)
+        if shard.gid_base:   # a replica: the same columns, its own global ids
+            seeds_like(rng, shard.gid)
+        return rays, rng
     return build
 
 
-def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks):
+def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks, gid_base: int = 0):
     """Host SoA columns + seeds of the global blocks ``blocks`` laid back to back (rays.build_rays
-    restricted to each run of consecutive blocks)."""
+    restricted to each run of consecutive blocks); ``gid_base`` offsets the global ids (a replica
+    shard)."""
     from .rays import build_rays, rng_seeds
     parts, seeds = [], []
     R = rays_per_fov
@@ -337,9 +376,12 @@ def shard_rays_host(points, num_fov_x, num_fov_y, lambdas, rays_per_fov, blocks)
         empty = build_rays(points, num_fov_x, num_fov_y, lambdas, R, blocks=(0, 0))
         return empty, rng_seeds(0, 0)
     rays = {k: np.concatenate([p[k] for p in parts]) for k in parts[0]}
-    return rays, np.concatenate(seeds)
+    seeds = np.concatenate(seeds)
+    if gid_base:
+        seeds_like(seeds, GidMap(gid_base + np.asarray(blocks, dtype=np.int64) * R, R))
+    return rays, seeds
 
 
-__all__ = ["block_range", "rank_blocks", "GidMap", "Shard", "make_shard", "slab_ids", "split_calls", "run_steps",
+__all__ = ["block_range", "rank_blocks", "GidMap", "Shard", "make_shard", "replica_shard", "seeds_like", "slab_ids", "split_calls", "run_steps",
            "reduce_eyebox", "EyeboxGather", "trace_job", "timed_run", "hip_tracer", "hip_shard_builder",
            "shard_rays_host", "MAX_TRACES_PER_CALL", "EB_SLAB", "SPILL"]
