@@ -39,7 +39,7 @@ int main() {
     hipEvent_t e0, e1;
     CHECK(hipEventCreate(&e0));
     CHECK(hipEventCreate(&e1));
-    const size_t spans[] = {(size_t)1 << 20, (size_t)16 << 20, (size_t)72 << 20, (size_t)512 << 20};
+    const size_t spans[] = {(size_t)1 << 20, (size_t)2 << 20, (size_t)4 << 20, (size_t)8 << 20, (size_t)72 << 20};
     std::mt19937_64 rng(1);
     for (size_t span : spans) {
         const uint32_t n = (uint32_t)(span / 4);
@@ -50,7 +50,7 @@ int main() {
         uint32_t *d = nullptr;
         CHECK(hipMalloc(&d, span));
         CHECK(hipMemcpy(d, perm.data(), span, hipMemcpyHostToDevice));
-        const int cfg[][2] = {{1, 1}, {1, 64}, {16, 16}, {16, 64}};   // {waves per CU, lanes}
+        const int cfg[][2] = {{1, 1}, {1, 64}, {4, 20}, {16, 20}, {16, 64}};   // {waves per CU, lanes}
         for (auto &c : cfg) {
             const int waves = c[0], lanes = c[1];
             const int wg = std::max(1, cus * waves / 4);
