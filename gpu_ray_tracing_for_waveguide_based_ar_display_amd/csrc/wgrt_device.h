@@ -20,13 +20,6 @@ namespace wgrt {
 // ----------------------------------------------------------------------------
 // The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t cell words (up to 32
 // polygons), uint32_t (up to 16 polygons: half the grid's cache footprint).
-// The stripe frame of a coupler's slices (row-interval locator, rl_pair): the unit normal of the
-// slice boundaries, the offset of the first boundary along it and the inverse slice width.
-struct RowFrame {
-    double nx, ny, b1, inv_h;
-    int jmax;   // slices - 2
-};
-
 template <class CellT>
 struct LocatorT {
     using Word = CellT;
@@ -38,9 +31,6 @@ struct LocatorT {
     double x0, y0, inv_h;
     int ncx, ncy;
     const double *bands;    // 128-B band records (LocatorHost::bands); NULL: CSR lists only
-    const uint4 *rows;      // row-interval records of the cell classes (wgrt_device.h rl_*), row_chunks per row
-    int row_chunks, oc_chunk0;
-    RowFrame fc_frame, oc_frame;
 };
 using Locator = LocatorT<uint64_t>;
 
@@ -610,10 +600,6 @@ struct JLane {
     uint32_t bounces;
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
-#if WGRT_ROWLOC
-    uint4 ra, rb;            // row-interval records of (x, y)'s cell row, loaded a step ahead ...
-    uint32_t rix;            // ... and the cell column they are decoded at
-#endif
     uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
 
@@ -762,57 +748,6 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
     iy = min(max(iy, 0), L.ncy - 1);
     return L.cells[iy * L.ncx + ix];
 }
-
-// Row-interval locator (32-bit cell words).  For a convex polygon the cells of one grid row that
-// are not OUT form one run, and its IN cells another, so a row of the cell grid is four column
-// bounds per polygon (row_bounds_kernel derives them from the cell words and checks that both
-// runs are contiguous, so decoding them gives exactly the cell word's classes).  The coupler
-// slices are parallel stripes (a convex hull cut into bands of a rotated frame, CC:313-320,
-// CC:408-452), so at a cell at most two consecutive slices are not OUT: the lane computes the pair
-// (j, j + 1) nearest its point from the stripe frame (rl_pair) and decodes only those two
-// (cover_kernel checks, for every cell, that the pair of any point in it covers every non-OUT
-// slice).  A row's record, 16-B chunks: [eff_reg1 | eff_reg2] [IC | -] [FC j | FC j + 1] for
-// j = 0 .. nfc - 2, [OC j | OC j + 1] for j = 0 .. noc - 2.  Per polygon: {lo = e_lo | in_lo << 16,
-// wp1 = (e_hi - e_lo + 1) | (in_hi - in_lo + 1) << 16}, an empty run wp1 = 0.  The table is ~200 B
-// per row (0.7 MB at C3): L2-resident, where the cell grid (71 MB) is not.
-typedef unsigned short wgrt_u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t rl_cls(uint32_t lo, uint32_t wp1, uint32_t ixx) {
-    const wgrt_u16x2 d = __builtin_bit_cast(wgrt_u16x2, ixx) - __builtin_bit_cast(wgrt_u16x2, lo);
-    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(wgrt_u16x2, wp1), d));
-    return (t >> 16) ? 1u : ((t & 0xffffu) ? 2u : 0u);
-}
-
-// the stripe pair (j, j + 1) of a point: the boundary between slices j and j + 1 nearest to it
-__device__ __forceinline__ int rl_pair(const RowFrame &f, double x, double y) {
-    const double t = floor((x * f.nx + y * f.ny - f.b1) * f.inv_h + 0.5);
-    return (int)fmin(fmax(t, 0.0), (double)f.jmax);
-}
-
-#if WGRT_ROWLOC
-// issue the row records of (x, y) for the coupler side the lane is on (oc: regions 4 / 5)
-template <class Loc>
-__device__ __forceinline__ void rl_issue(const Loc &L, JLane &J, double x, double y, bool oc) {
-    int ix = (int)((x - L.x0) * L.inv_h), iy = (int)((y - L.y0) * L.inv_h);
-    ix = min(max(ix, 0), L.ncx - 1);
-    iy = min(max(iy, 0), L.ncy - 1);
-    const int j = rl_pair(oc ? L.oc_frame : L.fc_frame, x, y);
-    const uint4 *rec = L.rows + (size_t)L.row_chunks * iy;
-    J.ra = rec[0];
-    J.rb = rec[(oc ? L.oc_chunk0 : 2) + j];
-    J.rix = (uint32_t)ix | ((uint32_t)j << 16);
-}
-
-// the cell word's classes of that side: eff_reg1, eff_reg2, and the side's slices j and j + 1
-__device__ __forceinline__ uint32_t rl_word(const JLane &J, bool oc, int nfc) {
-    const uint32_t ix = J.rix & 0xffffu, j = J.rix >> 16;
-    const uint32_t ixx = ix | (ix << 16);
-    const uint32_t w = rl_cls(J.ra.x, J.ra.y, ixx) | (rl_cls(J.ra.z, J.ra.w, ixx) << 2);
-    const uint32_t sh = 2u * ((oc ? 3u + (uint32_t)nfc : 3u) + j);
-    const uint32_t sl = rl_cls(J.rb.x, J.rb.y, ixx) | (rl_cls(J.rb.z, J.rb.w, ixx) << 2);
-    return w | (sl << sh);
-}
-#endif
 
 // |M E|^2 in single precision from the block's Hermitian form H = M^H M (the certified estimate
 // of a branch efficiency's numerator): h11 |Ete|^2 + h22 |Etm|^2 + 2 Re(h12 conj(Ete) Etm),
@@ -971,10 +906,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double2 mv = ba ? mva : mvb;
     r.x = r.x + mv.x;
     r.y = r.y + mv.y;
-#if WGRT_ROWLOC
-    if constexpr (sizeof(typename Loc::Word) == 4) rl_issue(loc, L, r.x, r.y, kind >= 3);
-    else
-#endif
     L.pf = locate_c(loc, r.x, r.y);
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
@@ -994,17 +925,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.gx = mv.x;
     r.gy = mv.y;
     if (kind == 0) {
-#if WGRT_ROWLOC
-        if constexpr (sizeof(typename Loc::Word) == 4) {
-            const int iy = min(max((int)((r.y - loc.y0) * loc.inv_h), 0), loc.ncy - 1);
-            const uint4 ic = loc.rows[(size_t)loc.row_chunks * iy + 1];
-            const uint32_t ix = L.rix & 0xffffu;
-            const typename Loc::Word wic = (typename Loc::Word)(rl_cls(ic.x, ic.y, ix | (ix << 16)) << (2 * kPolyIC));
-            const bool in_ic = in_poly_w<true>(loc, wic, kPolyIC, r.x, r.y);
-            if (ba) return in_ic ? 0 : 2;
-            return in_ic ? 1 : kDie;
-        }
-#endif
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
@@ -1056,15 +976,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
     constexpr W kLow = (W)0x5555555555555555ull;
     constexpr W kTop = (W)1 << (kBits - 1);
     JRay &r = L.r;
+    W c = (W)L.pf;
     const int region = r.region;
     const int nfc = A.nfc, noc = A.noc;
-#if WGRT_ROWLOC
-    W c;
-    if constexpr (sizeof(W) == 4) c = (W)rl_word(L, region >= 4, nfc);
-    else c = (W)L.pf;
-#else
-    W c = (W)L.pf;
-#endif
     // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
     const bool fc = region <= 3;
     const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
@@ -1098,17 +1012,8 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         r.x = r.x + r.gx;
         r.y = r.y + r.gy;
         ++r.hops;
-#if WGRT_ROWLOC
-        if constexpr (sizeof(W) == 4) rl_issue(loc, L, r.x, r.y, region >= 4);
-        else
-#endif
         L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
-#if WGRT_ROWLOC
-    // R3 -> R4 switch (no move): the next pass reads the OC side's classes of the same cell
-    if constexpr (sizeof(W) == 4)
-        if (sw) rl_issue(loc, L, r.x, r.y, true);
-#endif
     return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
 }
 
