@@ -176,13 +176,13 @@ def main(argv=None):
     else:
         collect = reduce_eyebox
 
-    def timed(steps, per_call):
+    def timed(steps, per_call, events=True):
         """steps chained traces as calls of per_call traces (distributed.timed_run: barrier, sync,
-        trace, eyebox collective, sync, barrier; time MAX and bounces SUM over ranks), with HIP
-        events around every call on the stream the kernels run on (torch's current stream)."""
+        trace, eyebox collective, sync, barrier; time MAX and bounces SUM over ranks); with events,
+        HIP events around every call on the stream the kernels run on (torch's current stream)."""
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
-              for _ in split_calls(steps, per_call)]
-        hook = lambda j, what: ev[j][0 if what == "start" else 1].record()
+              for _ in split_calls(steps, per_call)] if events else []
+        hook = (lambda j, what: ev[j][0 if what == "start" else 1].record()) if events else None
         elapsed, b_total, b_local = timed_run(tracer, rays, rng, eb, shard.gid, steps, per_call, stats,
                                               sync=torch.cuda.synchronize, hook=hook, collect=collect)
         check_stats(stats)
@@ -201,8 +201,12 @@ def main(argv=None):
     if not a.no_extras:
         run_steps(tracer, rays, rng, eb, shard.gid, 2, 0)
     torch.cuda.synchronize()
-    elapsed, bounces_total, bounces_local, call_ms = timed(a.steps, 1)
+    # the headline: K separate launches with nothing else on the stream; then the same K launches
+    # again with a HIP event pair around each, for the kernel duration the roofline divides by
+    # (event records between the launches would be part of the timed steps otherwise)
+    elapsed, bounces_total, bounces_local, _ = timed(a.steps, 1, events=False)
     value = bounces_total / elapsed
+    _el, _bt, ev_bounces_local, call_ms = timed(a.steps, 1)
     extras = {}
     if not a.no_extras:
         for key, steps, note in (("main_job", 4, "the reference's job: 4 chained traces (MAIN:169-177) as one call, "
@@ -214,14 +218,14 @@ def main(argv=None):
 
     if rank == 0:
         kavg_s = float(np.mean(call_ms)) / 1e3
-        achieved = bounces_local / len(call_ms) * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
+        achieved = ev_bounces_local / len(call_ms) * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
         sha = lib_sha16()
         traffic, traffic_note = None, "no PMC pass recorded for this library build"
         try:
             with open(a.traffic_json) as f:
                 ent = json.load(f).get(f"{cname}:v{a.variant}")
             if ent and ent.get("lib_sha16") == sha:
-                traffic = int(round(ent["bytes_per_bounce"] * bounces_local / len(call_ms)))
+                traffic = int(round(ent["bytes_per_bounce"] * ev_bounces_local / len(call_ms)))
                 traffic_note = ("rocprofv3 FETCH_SIZE + WRITE_SIZE of the trace kernel on this build (L2 <-> fabric "
                                 "bytes; Infinity-Cache hits included, so an upper bound on HBM bytes), per launch")
         except (OSError, ValueError, KeyError):
@@ -230,12 +234,14 @@ def main(argv=None):
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                     "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_note": traffic_note,
                     "kernel": kernel_name(a.variant, scene), "launch_avg_ms": round(kavg_s * 1e3, 4),
+                    "evented_ms_per_step": round(_el / a.steps * 1e3, 4),
                     "algo_bytes_per_bounce": ALGO_BYTES_PER_BOUNCE,
-                    "bounces_per_launch": int(round(bounces_local / len(call_ms))),
+                    "bounces_per_launch": int(round(ev_bounces_local / len(call_ms))),
                     "valu": valu if valu is not None else {
                         "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
                     "note": "launch_avg_ms: HIP events around each launch (trace kernel + its eyebox/replay "
-                            "epilogue kernel) on rank 0; valu: the issue-side bound SURVEY.md §8(d) calls binding "
+                            "epilogue kernel) on rank 0, in a second pass of the same K launches (the timed steps "
+                            "carry no event records); valu: the issue-side bound SURVEY.md §8(d) calls binding "
                             "(VALU busy = SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
