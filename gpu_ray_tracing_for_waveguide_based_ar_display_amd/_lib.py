@@ -15,7 +15,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 # WGRT_LIB: load another build of the library (A/B measurements of build variants, tools/ab.py)
 LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 # include/wgrt.h (the drop-in boundary) and include/wgrt_debug.h (test / profiling hooks)
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_create_ex", "wgrt_scene_destroy", "wgrt_scene_get_info",
             "wgrt_trace_fullcolor", "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex",
@@ -80,8 +80,11 @@ class LaunchOpts(ctypes.Structure):
                 ("debug", ctypes.POINTER(DebugOpts))]
 
 
+LUT_ORDER = ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1", "lut_fc2", "lut_oc1", "lut_oc2")   # lut_f32_angles bits
+
+
 class SceneOpts(ctypes.Structure):
-    _fields_ = [("cell_mm", ctypes.c_double), ("host_build", ctypes.c_int)]
+    _fields_ = [("cell_mm", ctypes.c_double), ("host_build", ctypes.c_int), ("lut_f32_angles", ctypes.c_int)]
 
 
 class ShadowStats(ctypes.Structure):
@@ -242,14 +245,21 @@ class Scene:
 
     def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
                  eff_reg_FOV_range, lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2,
-                 lut_TIR, lut_gap, device: int = 0, cell_mm: float = 0.0, host_build: bool = False):
-        """``cell_mm`` / ``host_build``: wgrt_scene_opts (0 / False: the defaults)."""
+                 lut_TIR, lut_gap, device: int = 0, cell_mm: float = 0.0, host_build: bool = False,
+                 lut_f32_angles: int | None = None):
+        """``cell_mm`` / ``host_build`` / ``lut_f32_angles``: wgrt_scene_opts (0 / False: the defaults;
+        ``lut_f32_angles=None``: bit k set for each LUT given in single precision, luts.lut_f32_mask)."""
         L = load()
         desc, _keep, (nl, nx, ny, nfc, noc) = make_desc(
             IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
             lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2, lut_TIR, lut_gap)
         h = _vp()
-        opts = SceneOpts(float(cell_mm), 1 if host_build else 0)
+        if lut_f32_angles is None:
+            from .luts import lut_f32_mask
+            lut_f32_angles = lut_f32_mask(dict(zip(LUT_ORDER, (lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2,
+                                                               lut_oc1, lut_oc2))))
+        opts = SceneOpts(float(cell_mm), 1 if host_build else 0, int(lut_f32_angles))
+        self.lut_f32_angles = int(lut_f32_angles)
         check(L.wgrt_scene_create_ex(ctypes.byref(desc), int(device), ctypes.byref(opts), ctypes.byref(h)),
               "wgrt_scene_create")
         self._h = h

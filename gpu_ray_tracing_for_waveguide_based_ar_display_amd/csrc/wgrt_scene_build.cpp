@@ -229,26 +229,30 @@ PackView pack_view(const wgrt_scene_desc &d, const double *trig) {
     return v;
 }
 
-void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig) {
+void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig, int lut_f32_angles) {
     const int nfc = (int)d.n_fc_slices, noc = (int)d.n_oc_slices;
     const int TG = trig_doubles(nfc, noc);
     const int64_t ntiles = (int64_t)d.num_lmd * d.nx * d.ny;
     trig.assign((size_t)ntiles * TG, 0.0);
     const PackView v = pack_view(d, nullptr);
+    // math.cos of table k's angle: libm cos, or cosf of the float32 angle for a complex64 table
+    auto lcos = [&](int k, double th) -> double {
+        return ((lut_f32_angles >> k) & 1) ? (double)std::cos((float)th) : std::cos(th);
+    };
     for (int64_t g = 0; g < ntiles; ++g) {
         const int64_t n = g % d.ny, m = g / d.ny % d.nx, l = g / ((int64_t)d.ny * d.nx);
         double *t = trig.data() + (size_t)g * TG;
         // math.cos of each LUT's polar angle (channel 0, real part; GRTF:868-1200)
-        t[0] = std::cos(lut_at(d.lut_ic1, 0, l, m, n, 0, v, v.ch5)[0]);
-        t[1] = std::cos(lut_at(d.lut_ic2, 0, l, m, n, 0, v, v.ch5)[0]);
-        t[2] = std::cos(lut_at(d.lut_ic3, 0, l, m, n, 0, v, v.ch5)[0]);
+        t[0] = lcos(0, lut_at(d.lut_ic1, 0, l, m, n, 0, v, v.ch5)[0]);
+        t[1] = lcos(1, lut_at(d.lut_ic2, 0, l, m, n, 0, v, v.ch5)[0]);
+        t[2] = lcos(2, lut_at(d.lut_ic3, 0, l, m, n, 0, v, v.ch5)[0]);
         for (int k = 0; k < nfc; ++k) {
-            t[3 + k] = std::cos(lut_at(d.lut_fc1, k, l, m, n, 0, v, v.ch3)[0]);
-            t[3 + nfc + k] = std::cos(lut_at(d.lut_fc2, k, l, m, n, 0, v, v.ch3)[0]);
+            t[3 + k] = lcos(3, lut_at(d.lut_fc1, k, l, m, n, 0, v, v.ch3)[0]);
+            t[3 + nfc + k] = lcos(4, lut_at(d.lut_fc2, k, l, m, n, 0, v, v.ch3)[0]);
         }
         for (int k = 0; k < noc; ++k) {
-            t[3 + 2 * nfc + k] = std::cos(lut_at(d.lut_oc1, k, l, m, n, 0, v, v.ch5)[0]);
-            t[3 + 2 * nfc + noc + k] = std::cos(lut_at(d.lut_oc2, k, l, m, n, 0, v, v.ch5)[0]);
+            t[3 + 2 * nfc + k] = lcos(5, lut_at(d.lut_oc1, k, l, m, n, 0, v, v.ch5)[0]);
+            t[3 + 2 * nfc + noc + k] = lcos(6, lut_at(d.lut_oc2, k, l, m, n, 0, v, v.ch5)[0]);
         }
         double *rot = t + 3 + 2 * nfc + 2 * noc;
         for (int k = 0; k < 4; ++k) {
@@ -311,7 +315,8 @@ void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys
     }
 }
 
-void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells, bool pack) {
+void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells, bool pack,
+                      int lut_f32_angles) {
     validate_desc(d);
     std::vector<const double *> polys;
     std::vector<int64_t> nv;
@@ -320,7 +325,7 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, 
         build_locator(polys, nv, cell_mm, out.loc);
     else
         build_locator_geometry(polys, nv, cell_mm, out.loc);
-    build_trig(d, out.trig);
+    build_trig(d, out.trig, lut_f32_angles);
     if (pack) {
         pack_tiles_host(d, out.trig, out.tiles, out.jtiles);
         // The kernels' cheap branch estimates assume finite tables (an inf / NaN coefficient would

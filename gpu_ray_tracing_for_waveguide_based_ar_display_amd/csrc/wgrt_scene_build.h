@@ -48,12 +48,14 @@ void classify_cells_host(const std::vector<const double *> &polys, const std::ve
 void build_locator(const std::vector<const double *> &polys, const std::vector<int64_t> &nverts,
                    double cell_mm, LocatorHost &out);
 PackView pack_view(const wgrt_scene_desc &d, const double *trig);
-void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig);
+// lut_f32_angles: wgrt_scene_opts bit mask of complex64 tables (cosf of their float32 angles)
+void build_trig(const wgrt_scene_desc &d, std::vector<double> &trig, int lut_f32_angles = 0);
 void pack_tiles_host(const wgrt_scene_desc &d, const std::vector<double> &trig, std::vector<double> &tiles,
                      std::vector<double> &jtiles);
 void validate_desc(const wgrt_scene_desc &d);
 // cells: classify the grid on the host; pack: pack the tiles on the host
-void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells = true, bool pack = true);
+void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, bool cells = true, bool pack = true,
+                      int lut_f32_angles = 0);
 // the polygon list the locator covers: eff_reg1, eff_reg2, IC, FC slices, OC slices
 void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys, std::vector<int64_t> &nv);
 

@@ -772,12 +772,14 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
     const double cell_mm = (opts && opts->cell_mm > 0.0) ? opts->cell_mm : kDefaultCellMm;
     if (opts && !(opts->cell_mm >= 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be >= 0");
     const bool host_build = opts && opts->host_build != 0;
+    const int f32_angles = opts ? opts->lut_f32_angles : 0;
+    if (f32_angles & ~0x7f) return fail(WGRT_ERR_INVALID_ARGUMENT, "lut_f32_angles has bits beyond the 7 LUTs");
     // host: validation, the locator's geometry (extent, vertices, row bands) and the trig table
     // (every cos / sin on the host libm); the cell words and the tiles are built on the device
     // (host_build: both on the host, the reference build the device one is checked against)
     SceneHost host;
     try {
-        build_scene_host(d, cell_mm, host, host_build, host_build);
+        build_scene_host(d, cell_mm, host, host_build, host_build, f32_angles);
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }

@@ -46,7 +46,7 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     from .couplers_coor import design_geometry
     from .distributed import EyeboxGather, hip_shard_builder, hip_tracer, make_shard, run_steps, split_calls
     from .engine import Scene, check_stats, new_stats, reserve
-    from .luts import load_luts, synthetic_luts, validate_luts
+    from .luts import load_luts, lut_f32_mask, synthetic_luts, validate_luts
     from .rays import generate_points_in_polygon
 
     world = dist.get_world_size() if dist.is_initialized() else 1
@@ -56,12 +56,14 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
 
     say("=" * 60 + "\nInitializing system components ...\n" + "=" * 60)
     geom = design_geometry(num_FOV_x, num_FOV_y)
+    f32_angles = 0
     if lut_dir:
-        luts = validate_luts(load_luts(lut_dir), len(geom.lmd), num_FOV_x, num_FOV_y, geom.num_fc_slices,
-                             geom.num_oc_slices)
+        raw = load_luts(lut_dir)
+        f32_angles = lut_f32_mask(raw)   # complex64 files: float32 cosines, as the compiled reference
+        luts = validate_luts(raw, len(geom.lmd), num_FOV_x, num_FOV_y, geom.num_fc_slices, geom.num_oc_slices)
     else:
         luts = synthetic_luts(geom, seed=lut_seed, profile=lut_profile)
-    scene = Scene.from_geometry(geom, luts, device=dev.index)
+    scene = Scene.from_geometry(geom, luts, device=dev.index, lut_f32_angles=f32_angles)
     R = int(num_rays_per_FoV)
     rng_pts = np.random.default_rng(point_seed) if point_seed is not None else None
     points = generate_points_in_polygon(geom.IC, R // 2, rng=rng_pts)

@@ -165,6 +165,19 @@ class LUTPrecisionWarning(UserWarning):
     """A LUT was given in single precision (complex64 / float32)."""
 
 
+def lut_f32_mask(luts: dict) -> int:
+    """wgrt_scene_opts.lut_f32_angles of a LUT set as given: bit k for each table k (ic1, ic2, ic3,
+    fc1, fc2, oc1, oc2) held in single precision.  The reference loads the .npy files as stored
+    (MAIN:28-34); compiled numba then takes math.cos of a complex64 table's float32 ``.real`` in
+    float32 (GRTF:866-869, ...), which the scene reproduces for the flagged tables."""
+    mask = 0
+    for k, name in enumerate(LUT_NAMES):
+        a = luts.get(name)
+        if a is not None and np.asarray(a).dtype in (np.complex64, np.float32, np.float16):
+            mask |= 1 << k
+    return mask
+
+
 def validate_luts(luts: dict, num_lmd: int, nx: int, ny: int, nfc: int, noc: int) -> dict:
     """Shape / dtype checks for a LUT set (real or synthetic); returns complex128 copies.
 
@@ -174,11 +187,13 @@ def validate_luts(luts: dict, num_lmd: int, nx: int, ny: int, nfc: int, noc: int
     Single-precision tables (complex64, as ``np.save`` of a complex64 array gives) are
     accepted and widened exactly to complex128, with a :class:`LUTPrecisionWarning`: the
     compiled reference kernel takes ``math.cos`` of a complex64 table's float32 ``.real``
-    (GRTF:866-869 and every cos ratio after it) in single precision, while the scene
-    builder here evaluates every cosine in double precision, so a draw lying within
-    float32 rounding of a branch threshold could be decided differently.  Parity with
-    the reference is pinned for complex128 tables only (the real files are not available
-    offline; their dtype is unknown).  The input dtypes are in ``validate_luts.last_dtypes``.
+    (GRTF:866-869 and every cos ratio after it) in single precision.  Pass
+    ``lut_f32_mask`` of the tables AS LOADED to the scene (``Scene(..., lut_f32_angles=mask)``;
+    the reference-flow driver does) and the scene takes those cosines as float32 ``cosf``
+    too.  Parity for such tables is pinned against the oracle's same semantics; against the
+    reference it is unpinned (CUDA's libdevice ``cosf`` and glibc's may differ in the last
+    bit, and the real files are not available offline).  The input dtypes are in
+    ``validate_luts.last_dtypes``.
     """
     want = {"lut_ic1": (num_lmd, nx, ny), "lut_ic2": (num_lmd, nx, ny), "lut_ic3": (num_lmd, nx, ny),
             "lut_fc1": (nfc, num_lmd, nx, ny), "lut_fc2": (nfc, num_lmd, nx, ny),
@@ -202,8 +217,9 @@ def validate_luts(luts: dict, num_lmd: int, nx: int, ny: int, nfc: int, noc: int
         out[name] = np.ascontiguousarray(a, dtype=np.complex128)
     validate_luts.last_dtypes = dtypes
     if single:
-        warnings.warn(f"single-precision LUTs {single} widened to complex128: parity with the reference "
-                      "is pinned for complex128 tables only (see validate_luts)", LUTPrecisionWarning, stacklevel=2)
+        warnings.warn(f"single-precision LUTs {single} widened to complex128: give the scene their lut_f32_mask so "
+                      "their angles' cosines are taken in float32 as compiled numba does (see validate_luts)",
+                      LUTPrecisionWarning, stacklevel=2)
     return out
 
 

@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 3
+#define WGRT_ABI_VERSION 4
 
 typedef enum {
     WGRT_OK = 0,
@@ -122,6 +122,13 @@ typedef struct {
     double cell_mm;   /* locator grid cell (mm); 0 = default 1/128 mm (fastest on C3) */
     int host_build;   /* 1: build the cell words and tiles on the host (the reference the device build
                          is checked against; slow); 0: on the device                              */
+    int lut_f32_angles;   /* ABI 4.  Bit k set: LUT k (lut_ic1, ic2, ic3, fc1, fc2, oc1, oc2) was a
+                             complex64 table in the reference's run (MAIN:28-34 loads the .npy files as
+                             stored).  Compiled numba takes math.cos of a complex64 table's float32 .real
+                             in single precision (GRTF:866-869 and every cos ratio after it), so the
+                             scene's cosines of that table's angles are cosf of the float32 angle,
+                             widened.  The coefficients themselves enter E_field_cal widened exactly, as
+                             numba promotes complex64 x complex128.  0: double-precision cos (complex128). */
 } wgrt_scene_opts;
 wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const wgrt_scene_opts *opts,
                                  wgrt_scene **out);

@@ -40,7 +40,7 @@ class _Scene(ctypes.Structure):
         ("fc1", _f64p), ("fc2", _f64p), ("oc1", _f64p), ("oc2", _f64p),
         ("num_lmd", ctypes.c_int32), ("nx", ctypes.c_int32), ("ny", ctypes.c_int32),
         ("ch5", ctypes.c_int32), ("ch3", ctypes.c_int32),
-        ("n_g", ctypes.c_double), ("threshold", ctypes.c_double),
+        ("n_g", ctypes.c_double), ("threshold", ctypes.c_double), ("f32_mask", ctypes.c_int32),
     ]
 
 
@@ -102,7 +102,9 @@ class OracleScene:
     """Geometry + LUT arrays in the reference's layout, held alive for the C side."""
 
     def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
-                 eff_reg_FOV_range, luts: dict, lut_TIR, lut_gap):
+                 eff_reg_FOV_range, luts: dict, lut_TIR, lut_gap, f32_mask: int = 0):
+        """``f32_mask``: bit k set = LUT k (ic1, ic2, ic3, fc1, fc2, oc1, oc2) is complex64 in the
+        reference's run, whose compiled kernel takes the cosine of its float32 angles in float32."""
         c = lambda a, dt=np.float64: np.ascontiguousarray(a, dtype=dt)
         # single-wavelength LUT shapes (GRTF:419-427): lut_TIR [NX, NY, 4], ... -> lambda axis of 1
         self.single_lambda = np.ndim(lut_TIR) == 3
@@ -131,10 +133,10 @@ class OracleScene:
             *[k[n].ctypes.data_as(_f64p) for n in ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1",
                                                    "lut_fc2", "lut_oc1", "lut_oc2")],
             L, NX, NY, k["lut_ic1"].shape[-1], k["lut_fc1"].shape[-1], float(n_g),
-            1e-15 if self.single_lambda else 0.0)
+            1e-15 if self.single_lambda else 0.0, int(f32_mask))
 
     @classmethod
-    def from_geometry(cls, geom, luts, wavelength: int | None = None):
+    def from_geometry(cls, geom, luts, wavelength: int | None = None, f32_mask: int = 0):
         """``wavelength=l``: the single-wavelength scene of wavelength l (process_rays_kernel_pro)."""
         tir, gap = geom.lut_TIR, geom.lut_gap
         if wavelength is not None:
@@ -142,7 +144,7 @@ class OracleScene:
                     for k, v in luts.items() if k.startswith("lut_")}
             tir, gap = tir[wavelength], gap[wavelength]
         return cls(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g, geom.eff_reg1,
-                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts, tir, gap)
+                   geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range, luts, tir, gap, f32_mask=f32_mask)
 
     def eb_shape(self):
         if self.single_lambda:

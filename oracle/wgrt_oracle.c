@@ -151,9 +151,18 @@ static const cplx *lut3(const wgrt_oracle_scene *sc, const double *lut, int64_t 
     return (const cplx *)(lut + 2 * idx);
 }
 
-/* Take branch: update field, direction, position (the common block of every branch). */
-static void take(ray_state *st, const efield *E, double theta_re, double tir, const double *gap2) {
-    st->cos_th = cos(theta_re);
+/* math.cos(lut[..., 0].real) of table k (GRTF:866-869, 917-918, ...): double cos of a complex128
+ * table's angle; for a complex64 table (f32_mask bit k) compiled numba types the float32 .real's
+ * cosine as float32, i.e. cosf of the float32 angle. */
+enum { T_IC1, T_IC2, T_IC3, T_FC1, T_FC2, T_OC1, T_OC2 };
+static double lcos(const wgrt_oracle_scene *sc, int k, double th) {
+    return ((sc->f32_mask >> k) & 1) ? (double)cosf((float)th) : cos(th);
+}
+
+/* Take branch: update field, direction, position (the common block of every branch);
+ * cos_theta = math.cos of the new direction's angle (lcos). */
+static void take(ray_state *st, const efield *E, double cos_theta, double tir, const double *gap2) {
+    st->cos_th = cos_theta;
     double norm = sqrt(E->te * E->te + E->tm * E->tm);
     double ph = efield_phase(E);
     st->Ete = E->te / norm;
@@ -212,15 +221,15 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                    lut5(sc, sc->ic1, 0, l, m, n, 33), lut5(sc, sc->ic1, 0, l, m, n, 38), &E1);
         efield_amp(st.Ete, st.Etm, cd, sd, lut5(sc, sc->ic1, 0, l, m, n, 15), lut5(sc, sc->ic1, 0, l, m, n, 20),
                    lut5(sc, sc->ic1, 0, l, m, n, 35), lut5(sc, sc->ic1, 0, l, m, n, 40), &E2);
-        double e1 = (E1.te * E1.te + E1.tm * E1.tm) * cos(th_ic2) / cos(th_ic1) * n_g;
-        double e2 = (E2.te * E2.te + E2.tm * E2.tm) * cos(th_ic3) / cos(th_ic1) * n_g;
+        double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_IC2, th_ic2) / lcos(sc, T_IC1, th_ic1) * n_g;
+        double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_IC3, th_ic3) / lcos(sc, T_IC1, th_ic1) * n_g;
         double u = rng_draw(&s, gid);
         if (u <= e1) {
-            take(&st, &E1, th_ic2, tir[0], gap + 0);
+            take(&st, &E1, lcos(sc, T_IC2, th_ic2), tir[0], gap + 0);
             st.ener *= e1;
             region = inside_or_on_edge(st.x, st.y, sc->ic, sc->n_ic) ? 0 : 2;
         } else if (u <= e1 + e2) {
-            take(&st, &E2, th_ic3, tir[2], gap + 4);
+            take(&st, &E2, lcos(sc, T_IC3, th_ic3), tir[2], gap + 4);
             st.ener *= e2;
             if (!inside_or_on_edge(st.x, st.y, sc->ic, sc->n_ic)) { why = 96; goto done; }
             region = 1;
@@ -248,15 +257,15 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 efield_amp(st.Ete, st.Etm, cd, sd, lut5(sc, L, 0, l, m, n, 4), lut5(sc, L, 0, l, m, n, 9),
                            lut5(sc, L, 0, l, m, n, 24), lut5(sc, L, 0, l, m, n, 29), &E2);
             }
-            double e1 = (E1.te * E1.te + E1.tm * E1.tm) * cos(th_ic2) / st.cos_th;
-            double e2 = (E2.te * E2.te + E2.tm * E2.tm) * cos(th_ic3) / st.cos_th;
+            double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_IC2, th_ic2) / st.cos_th;
+            double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_IC3, th_ic3) / st.cos_th;
             double u = rng_draw(&s, gid);
             if (u <= e1) {
-                take(&st, &E1, th_ic2, tir[0], gap + 0);
+                take(&st, &E1, lcos(sc, T_IC2, th_ic2), tir[0], gap + 0);
                 st.ener *= e1;
                 region = inside_or_on_edge(st.x, st.y, sc->ic, sc->n_ic) ? 0 : 2;
             } else if (u <= e1 + e2) {
-                take(&st, &E2, th_ic3, tir[2], gap + 4);
+                take(&st, &E2, lcos(sc, T_IC3, th_ic3), tir[2], gap + 4);
                 st.ener *= e2;
                 if (!inside_or_on_edge(st.x, st.y, sc->ic, sc->n_ic)) { why = (uint8_t)(10 * region + 6); goto done; }
                 region = 1;
@@ -286,16 +295,16 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                     efield_amp(st.Ete, st.Etm, cd, sd, lut3(sc, L, k, l, m, n, 3), lut3(sc, L, k, l, m, n, 6),
                                lut3(sc, L, k, l, m, n, 15), lut3(sc, L, k, l, m, n, 18), &E2);
                 }
-                double e1 = (E1.te * E1.te + E1.tm * E1.tm) * cos(th1) / st.cos_th;
-                double e2 = (E2.te * E2.te + E2.tm * E2.tm) * cos(th2) / st.cos_th;
+                double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_FC1, th1) / st.cos_th;
+                double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_FC2, th2) / st.cos_th;
                 double en1 = st.ener * e1, en2 = st.ener * e2;
                 double u = rng_draw(&s, gid);
                 if (u <= e1 && en1 > sc->threshold) {
-                    take(&st, &E1, th1, tir[0], gap + 0);
+                    take(&st, &E1, lcos(sc, T_FC1, th1), tir[0], gap + 0);
                     st.ener = en1 * 1.0;
                     region = 2;
                 } else if (u <= e1 + e2 && en2 > sc->threshold) {
-                    take(&st, &E2, th2, tir[1], gap + 2);
+                    take(&st, &E2, lcos(sc, T_FC2, th2), tir[1], gap + 2);
                     st.ener = en2 * 1.0;
                     region = 3;
                 } else {
@@ -343,17 +352,17 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                     efield_amp(st.Ete, st.Etm, cd, sd, lut5(sc, L, k, l, m, n, 15), lut5(sc, L, k, l, m, n, 20),
                                lut5(sc, L, k, l, m, n, 35), lut5(sc, L, k, l, m, n, 40), &E3);
                 }
-                double e1 = (E1.te * E1.te + E1.tm * E1.tm) * cos(th1) / st.cos_th;
-                double e2 = (E2.te * E2.te + E2.tm * E2.tm) * cos(th2) / st.cos_th;
-                double e3 = (E3.te * E3.te + E3.tm * E3.tm) * cos(th_ic1) / st.cos_th / n_g;
+                double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_OC1, th1) / st.cos_th;
+                double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_OC2, th2) / st.cos_th;
+                double e3 = (E3.te * E3.te + E3.tm * E3.tm) * lcos(sc, T_IC1, th_ic1) / st.cos_th / n_g;
                 double en1 = st.ener * e1, en2 = st.ener * e2, en3 = st.ener * e3;
                 double u = rng_draw(&s, gid);
                 if (u <= e1 && en1 > sc->threshold) {
-                    take(&st, &E1, th1, tir[1], gap + 2);
+                    take(&st, &E1, lcos(sc, T_OC1, th1), tir[1], gap + 2);
                     st.ener = en1 * 1.0;
                     region = 4;
                 } else if (u <= e1 + e2 && en2 > sc->threshold) {
-                    take(&st, &E2, th2, tir[3], gap + 6);
+                    take(&st, &E2, lcos(sc, T_OC2, th2), tir[3], gap + 6);
                     st.ener = en2 * 1.0;
                     region = 5;
                 } else if (u <= e1 + e2 + e3 && en3 > sc->threshold) {

@@ -27,6 +27,8 @@ typedef struct {
     double n_g;
     double threshold;   /* R2..R5 guard ener * eff > threshold: 0 full colour (GRTF:859),
                            1e-15 single wavelength (GRTF:444) */
+    int32_t f32_mask;   /* bit k: table k (ic1, ic2, ic3, fc1, fc2, oc1, oc2) was complex64, so compiled
+                           numba takes math.cos of its float32 .real in single precision (cosf) */
 } wgrt_oracle_scene;
 
 typedef struct {

@@ -72,3 +72,23 @@ class GoldenCase:
         eb = np.zeros(self.eb_shape(), np.float32)
         eb.reshape(-1)[self.f[f"eb_idx_after{after}"]] = self.f[f"eb_val_after{after}"]
         return eb
+
+
+def complex64_case(nx=3, ny=3, lambdas=(0, 1, 2), R=64):
+    """A LUT set held in complex64 (as np.save of complex64 tables gives) on which the reference's
+    single-precision cosine of a float32 angle (compiled numba: math.cos of a complex64 ``.real``,
+    GRTF:866-869) changes a decision: ray 0 (TE, tile (0, 0, 0)) in-couples with e1 = |c13|^2 *
+    cos(theta_ic2) / cos(theta_ic1) * n_g, theta_ic1 = 0 and theta_ic2 = float32(0.7000002), c13 = a,
+    c18 = 0, where a is chosen so that its first draw u = 0.316593... lies between e1 with cosf and
+    e1 with cos (libm values 0.76484203338623 / 0.76484204137068).  Returns (geom, luts, rays)."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, generate_points_in_polygon
+    geom = design_geometry(nx, ny)
+    luts = {k: np.asarray(v).astype(np.complex64) for k, v in synthetic_luts(geom, seed=0).items()}
+    luts["lut_ic1"][..., 0] = 0.0
+    luts["lut_ic1"][0, 0, 0, 13] = np.float32(0.46675431728363037)
+    luts["lut_ic1"][0, 0, 0, 18] = 0.0
+    luts["lut_ic2"][0, 0, 0, 0] = np.float32(0.7000002264976501)
+    pts = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(1))
+    return geom, luts, build_rays(pts, nx, ny, list(lambdas), R)
