@@ -51,7 +51,10 @@ namespace {
 
 // Cell size (mm) of the global-memory locator grid (wgrt_scene_opts.cell_mm = 0): 1/128 mm, a 71 MB
 // grid at C3; fewer EDGE-cell exact tests than coarser grids (fastest on C3).
-constexpr double kDefaultCellMm = 0.0078125;
+#ifndef WGRT_CELL_MM
+#define WGRT_CELL_MM 0.0078125
+#endif
+constexpr double kDefaultCellMm = WGRT_CELL_MM;
 
 
 #define HIP_TRY(expr)                                                                       \
