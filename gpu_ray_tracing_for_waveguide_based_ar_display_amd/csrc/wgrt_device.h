@@ -20,13 +20,6 @@ namespace wgrt {
 // ----------------------------------------------------------------------------
 // The exact polygon locator (wgrt_scene_build.cpp).  CellT = uint64_t cell words (up to 32
 // polygons), uint32_t (up to 16 polygons: half the grid's cache footprint).
-// The stripe frame of a coupler's slices (row-interval locator, rl_pair): the unit normal of the
-// slice boundaries, the offset of the first boundary along it and the inverse slice width.
-struct RowFrame {
-    double nx, ny, b1, inv_h;
-    int jmax;   // slices - 2
-};
-
 template <class CellT>
 struct LocatorT {
     using Word = CellT;
@@ -38,9 +31,6 @@ struct LocatorT {
     double x0, y0, inv_h;
     int ncx, ncy;
     const double *bands;    // 128-B band records (LocatorHost::bands); NULL: CSR lists only
-    const uint4 *rows;      // row-interval records of the cell classes (rl_*), row_chunks per row; NULL: none
-    int row_chunks, oc_chunk0;
-    RowFrame fc_frame, oc_frame;
 };
 using Locator = LocatorT<uint64_t>;
 
@@ -610,10 +600,7 @@ struct JLane {
     uint32_t bounces;
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
-    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead ...
-    uint4 ra, rb;            // ... or (launch tail, rl_issue) the row-interval records of its cell row
-    uint32_t rix;            // and the cell column | stripe pair << 16 they are decoded at
-    bool rows;               // the pending lookup is ra / rb (else pf)
+    uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
 };
 
 enum : int { kUncertain = -3, kOut = -4 };
@@ -763,69 +750,6 @@ __device__ __forceinline__ typename Loc::Word locate_c(const Loc &L, double x, d
     return L.cells[iy * L.ncx + ix];
 }
 
-// Row-interval locator (32-bit cell words; the launch tail's lookups).  For a convex polygon the
-// cells of one grid row that are not OUT form one run, and its IN cells another, so a row of the
-// cell grid is four column bounds per polygon (row_bounds_kernel derives them from the cell words
-// and checks that both runs are contiguous, so decoding them gives exactly the cell word's
-// classes).  The coupler slices are parallel stripes (a convex hull cut into bands of a rotated
-// frame, CC:313-320, CC:408-452), so at a cell at most two consecutive slices are not OUT: the lane
-// computes the pair (j, j + 1) nearest its point from the stripe frame (rl_pair) and decodes only
-// those two (cover_kernel checks, for every cell, that the pair of any point in it covers every
-// non-OUT slice).  A row's record, 16-B chunks: [eff_reg1 | eff_reg2] [IC | -] [FC j | FC j + 1] for
-// j = 0 .. nfc - 2, [OC j | OC j + 1] for j = 0 .. noc - 2.  Per polygon: {lo = e_lo | in_lo << 16,
-// wp1 = (e_hi - e_lo + 1) | (in_hi - in_lo + 1) << 16}, an empty run wp1 = 0.  The table is ~200 B
-// per row (0.7 MB at C3): L2-resident, where the cell grid (71 MB) is not -- a dependent lookup at
-// L2 latency instead of the Infinity Cache's, at the price of two loads and ~40 decode
-// instructions: slower while the chip is full, used once a wave's queue ran dry.
-typedef unsigned short wgrt_u16x2 __attribute__((ext_vector_type(2)));
-
-__device__ __forceinline__ uint32_t rl_cls(uint32_t lo, uint32_t wp1, uint32_t ixx) {
-    const wgrt_u16x2 d = __builtin_bit_cast(wgrt_u16x2, ixx) - __builtin_bit_cast(wgrt_u16x2, lo);
-    const uint32_t t = __builtin_bit_cast(uint32_t, __builtin_elementwise_sub_sat(__builtin_bit_cast(wgrt_u16x2, wp1), d));
-    return (t >> 16) ? 1u : ((t & 0xffffu) ? 2u : 0u);
-}
-
-// the stripe pair (j, j + 1) of a point: the boundary between slices j and j + 1 nearest to it
-__device__ __forceinline__ int rl_pair(const RowFrame &f, double x, double y) {
-    const double t = floor((x * f.nx + y * f.ny - f.b1) * f.inv_h + 0.5);
-    return (int)fmin(fmax(t, 0.0), (double)f.jmax);
-}
-
-// issue the row records of (x, y) for the coupler side the lane is on (oc: regions 4 / 5)
-template <class Loc>
-__device__ __forceinline__ void rl_issue(const Loc &L, JLane &J, double x, double y, bool oc) {
-    int ix = (int)((x - L.x0) * L.inv_h), iy = (int)((y - L.y0) * L.inv_h);
-    ix = min(max(ix, 0), L.ncx - 1);
-    iy = min(max(iy, 0), L.ncy - 1);
-    const int j = rl_pair(oc ? L.oc_frame : L.fc_frame, x, y);
-    const uint4 *rec = L.rows + (size_t)L.row_chunks * iy;
-    J.ra = rec[0];
-    J.rb = rec[(oc ? L.oc_chunk0 : 2) + j];
-    J.rix = (uint32_t)ix | ((uint32_t)j << 16);
-    J.rows = true;
-}
-
-// the cell word's classes of that side: eff_reg1, eff_reg2, and the side's slices j and j + 1
-__device__ __forceinline__ uint32_t rl_word(const JLane &J, bool oc, int nfc) {
-    const uint32_t ix = J.rix & 0xffffu, j = J.rix >> 16;
-    const uint32_t ixx = ix | (ix << 16);
-    const uint32_t w = rl_cls(J.ra.x, J.ra.y, ixx) | (rl_cls(J.ra.z, J.ra.w, ixx) << 2);
-    const uint32_t sh = 2u * ((oc ? 3u + (uint32_t)nfc : 3u) + j);
-    const uint32_t sl = rl_cls(J.rb.x, J.rb.y, ixx) | (rl_cls(J.rb.z, J.rb.w, ixx) << 2);
-    return w | (sl << sh);
-}
-
-// the cell lookup of a lane's new position (read by the next pass): the grid word, or (rows, a
-// wave-uniform mode: the launch tail) the row records
-template <class Loc>
-__device__ __forceinline__ void lookup(const Loc &L, JLane &J, double x, double y, bool oc, bool rows) {
-    if (sizeof(typename Loc::Word) == 4 && rows) {
-        rl_issue(L, J, x, y, oc);
-    } else {
-        J.pf = locate_c(L, x, y);   // (the tail clears J.rows once for the lookups the main loop left)
-    }
-}
-
 // |M E|^2 in single precision from the block's Hermitian form H = M^H M (the certified estimate
 // of a branch efficiency's numerator): h11 |Ete|^2 + h22 |Etm|^2 + 2 Re(h12 conj(Ete) Etm),
 // with a = |Ete|^2, b = |Etm|^2, (cr, ci) = conj(Ete) Etm shared by every branch.
@@ -929,7 +853,7 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // are the same values the all-double evaluation gives.
 template <bool SINGLE, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
-                                        bool entry, bool rows = false) {
+                                        bool entry) {
     JRay &r = L.r;
     const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
@@ -973,7 +897,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double2 mv = ba ? mva : mvb;
     r.x = r.x + mv.x;
     r.y = r.y + mv.y;
-    lookup(loc, L, r.x, r.y, kind >= 3, rows);
+    L.pf = locate_c(loc, r.x, r.y);
     // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
     // in-coupler states and R5 never hop), loaded with the taken branch's matrix
     const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
@@ -997,14 +921,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.hr = hop.x;
     r.hi = hop.y;
     if (kind == 0) {
-        typename Loc::Word wic = (typename Loc::Word)L.pf;
-        if (sizeof(typename Loc::Word) == 4 && rows) {
-            const int iy = min(max((int)((r.y - loc.y0) * loc.inv_h), 0), loc.ncy - 1);
-            const uint4 ic = loc.rows[(size_t)loc.row_chunks * iy + 1];
-            const uint32_t ix = L.rix & 0xffffu;
-            wic = (typename Loc::Word)(rl_cls(ic.x, ic.y, ix | (ix << 16)) << (2 * kPolyIC));
-        }
-        const bool in_ic = in_poly_w<true>(loc, wic, kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -1049,16 +966,15 @@ __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); 
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
 template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind, bool rows = false) {
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
     constexpr W kTop = (W)1 << (kBits - 1);
     JRay &r = L.r;
+    W c = (W)L.pf;
     const int region = r.region;
     const int nfc = A.nfc, noc = A.noc;
-    W c = (W)L.pf;
-    if (sizeof(W) == 4 && rows && L.rows) c = (W)rl_word(L, region >= 4, nfc);
     // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
     const bool fc = region <= 3;
     const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
@@ -1097,10 +1013,8 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
         const double mr = r.mr;
         r.mr = fma(mr, r.hr, -r.mi * r.hi);
         r.mi = fma(mr, r.hi, r.mi * r.hr);
-        lookup(loc, L, r.x, r.y, region >= 4, rows);   // read by the next pass
+        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
-    // R3 -> R4 switch (no move): with row records the next pass needs the OC side's of the same cell
-    if (sizeof(W) == 4 && rows && sw) rl_issue(loc, L, r.x, r.y, true);
     return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
 }
 

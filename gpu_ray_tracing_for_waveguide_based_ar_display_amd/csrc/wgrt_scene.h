@@ -19,9 +19,6 @@ struct wgrt_scene {
     int jtile_d = 0;
     uint64_t *d_cells = nullptr;
     uint32_t *d_cells32 = nullptr;   // 32-bit copy of the cell words (npoly <= 16), else NULL
-    uint4 *d_rows = nullptr;         // row-interval records of the 32-bit cell words (build_rows), or NULL
-    int row_chunks = 0, oc_chunk0 = 0;
-    wgrt::RowFrame fc_frame{}, oc_frame{};
     double *d_verts = nullptr;
     int32_t *d_poly_off = nullptr;
     int32_t *d_row_off = nullptr;
@@ -69,11 +66,6 @@ inline Locator make_locator(const wgrt_scene *s) {
     L.row_off = s->d_row_off;
     L.row_edges = s->d_row_edges;
     L.bands = s->d_bands;
-    L.rows = s->d_rows;
-    L.row_chunks = s->row_chunks;
-    L.oc_chunk0 = s->oc_chunk0;
-    L.fc_frame = s->fc_frame;
-    L.oc_frame = s->oc_frame;
     L.x0 = s->loc_host.x0;
     L.y0 = s->loc_host.y0;
     L.inv_h = s->loc_host.inv_h;
@@ -91,8 +83,6 @@ inline LocatorT<uint32_t> make_locator32(const wgrt_scene *s) {
     L.row_off = g.row_off;
     L.row_edges = g.row_edges;
     L.bands = g.bands;
-    L.rows = g.rows;
-    L.row_chunks = g.row_chunks, L.oc_chunk0 = g.oc_chunk0, L.fc_frame = g.fc_frame, L.oc_frame = g.oc_frame;
     L.x0 = g.x0, L.y0 = g.y0, L.inv_h = g.inv_h, L.ncx = g.ncx, L.ncy = g.ncy;
     return L;
 }

@@ -29,7 +29,6 @@
 #include <mutex>
 #include <string>
 #include <vector>
-#include <type_traits>
 
 #include "../../include/wgrt.h"
 #include "../../include/wgrt_debug.h"
@@ -331,14 +330,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     // the second half of a pass: the interaction of the lanes at one, then this pass's
     // out-couplings into the wave's block of queue slots (a contended returning atomic per pass
     // would put its latency on every pass; a new block is needed about once per hundred passes)
-    auto interact_pass = [&](bool rows) {
+    auto interact_pass = [&]() {
         if (TL && tl_on) {
             ++tl_passes;
             tl_lanes += __popcll(__ballot(active));
         }
         bool out = false;
         if (active && blk >= 0) {
-            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry, rows);
+            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
                 retire();
@@ -488,7 +487,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
         // the tail loop below
         if (!FUSED && exhausted) break;
-        interact_pass(false);
+        interact_pass();
     }
     if (!FUSED && __ballot(active) != 0ull) {
         // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
@@ -497,24 +496,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // cell words before the decision here (one or two round trips less per interaction) lost
         // 1.5 % and 6 %: the chip is still full of rays when the queue runs dry.
         // The first pass continues the one the main loop broke off (advance and refill done).
-        // With the scene's row-interval records (wgrt_device.h rl_*) the tail's cell lookups are
-        // answered from that L2-resident table instead of the 71 MB grid: the launch tail is bound
-        // by each ray's chain of dependent loads, not by the instructions the chip issues.
-        bool rows = false;
-#if WGRT_TAIL_ROWS
-        if (loc.rows) {
-            rows = true;
-            L.rows = false;   // the lookups the main loop left are grid words
-        }
-#endif
         for (bool first = true;; first = false) {
             if (!first && active) {
-                blk = advance(A, loc, L, kind, rows);
+                blk = advance(A, loc, L, kind);
                 entry = false;
                 if (blk == kDie) retire();
             }
             if (__ballot(active) == 0ull) break;
-            interact_pass(rows);
+            interact_pass();
         }
     }
     // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one
@@ -772,182 +761,6 @@ wgrt_status upload(const std::vector<T> &v, T **dst) {
 
 }  // namespace
 
-#ifndef WGRT_TAIL_ROWS
-#define WGRT_TAIL_ROWS 1
-#endif
-
-// Row-interval records of the 32-bit cell words (wgrt_device.h rl_*): one workgroup per cell row.
-// For every polygon the row's non-OUT cells and its IN cells must each form one run; a row breaking
-// that sets *bad and the scene keeps the plain cell grid.
-__global__ __launch_bounds__(256) void row_bounds_kernel(const uint32_t *cells, int ncx, int nfc, int noc,
-                                                         int row_chunks, uint4 *rows, int *bad) {
-    __shared__ int mn_e[16], mx_e[16], cn_e[16], mn_i[16], mx_i[16], cn_i[16];
-    const int row = blockIdx.x, npoly = 3 + nfc + noc;
-    if (threadIdx.x < 16) {
-        mn_e[threadIdx.x] = mn_i[threadIdx.x] = 0x7fffffff;
-        mx_e[threadIdx.x] = mx_i[threadIdx.x] = -1;
-        cn_e[threadIdx.x] = cn_i[threadIdx.x] = 0;
-    }
-    __syncthreads();
-    for (int ix = threadIdx.x; ix < ncx; ix += blockDim.x) {
-        const uint32_t w = cells[(size_t)row * ncx + ix];
-        for (int k = 0; k < npoly; ++k) {
-            const uint32_t c = (w >> (2 * k)) & 3u;
-            if (c) {
-                atomicMin(&mn_e[k], ix);
-                atomicMax(&mx_e[k], ix);
-                atomicAdd(&cn_e[k], 1);
-            }
-            if (c == 1u) {
-                atomicMin(&mn_i[k], ix);
-                atomicMax(&mx_i[k], ix);
-                atomicAdd(&cn_i[k], 1);
-            }
-        }
-    }
-    __syncthreads();
-    if (threadIdx.x != 0) return;
-    bool ok = true;
-    for (int k = 0; k < npoly; ++k) {
-        ok = ok && (cn_e[k] == 0 || cn_e[k] == mx_e[k] - mn_e[k] + 1);
-        ok = ok && (cn_i[k] == 0 || cn_i[k] == mx_i[k] - mn_i[k] + 1);
-    }
-    auto pack = [&](int k) -> uint2 {
-        if (cn_e[k] == 0) return make_uint2(0xffffffffu, 0u);
-        const uint32_t ilo = cn_i[k] ? (uint32_t)mn_i[k] : 0xffffu;
-        const uint32_t iw = cn_i[k] ? (uint32_t)(mx_i[k] - mn_i[k] + 1) : 0u;
-        return make_uint2((uint32_t)mn_e[k] | (ilo << 16), (uint32_t)(mx_e[k] - mn_e[k] + 1) | (iw << 16));
-    };
-    uint4 *r = rows + (size_t)row_chunks * row;
-    const uint2 e1 = pack(0), e2 = pack(1), ic = pack(2);
-    r[0] = make_uint4(e1.x, e1.y, e2.x, e2.y);
-    r[1] = make_uint4(ic.x, ic.y, 0u, 0u);
-    int c = 2;
-    for (int j = 0; j + 1 < nfc; ++j, ++c) {
-        const uint2 p = pack(3 + j), q = pack(4 + j);
-        r[c] = make_uint4(p.x, p.y, q.x, q.y);
-    }
-    for (int j = 0; j + 1 < noc; ++j, ++c) {
-        const uint2 p = pack(3 + nfc + j), q = pack(4 + nfc + j);
-        r[c] = make_uint4(p.x, p.y, q.x, q.y);
-    }
-    if (!ok) atomicOr(bad, 1);
-}
-
-// Every cell: the non-OUT slices of each coupler lie in the pair (j, j + 1) that rl_pair gives any
-// point of the cell (its corners, widened by 1e-9 mm, bound j: rl_pair is monotone in x and y).
-__global__ __launch_bounds__(256) void cover_kernel(const uint32_t *cells, int ncx, int ncy, double x0, double y0,
-                                                    double h, int nfc, int noc, RowFrame ff, RowFrame of, int *bad) {
-    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= (int64_t)ncx * ncy) return;
-    const int ix = (int)(i % ncx), iy = (int)(i / ncx);
-    const uint32_t w = cells[i];
-    const double xa = x0 + ix * h - 1e-9, xb = x0 + (ix + 1) * h + 1e-9;
-    const double ya = y0 + iy * h - 1e-9, yb = y0 + (iy + 1) * h + 1e-9;
-    auto check = [&](const RowFrame &f, int first, int count) -> bool {
-        uint32_t m = 0;
-        for (int k = 0; k < count; ++k)
-            if ((w >> (2 * (first + k))) & 3u) m |= 1u << k;
-        if (!m) return true;
-        const int j0 = min(min(rl_pair(f, xa, ya), rl_pair(f, xa, yb)), min(rl_pair(f, xb, ya), rl_pair(f, xb, yb)));
-        const int j1 = max(max(rl_pair(f, xa, ya), rl_pair(f, xa, yb)), max(rl_pair(f, xb, ya), rl_pair(f, xb, yb)));
-        for (int j = j0; j <= j1; ++j)
-            if (m & ~(3u << j)) return false;
-        return true;
-    };
-    if (!check(ff, 3, nfc) || !check(of, 3 + nfc, noc)) atomicOr(bad, 1);
-}
-
-// The stripe frame of slices first .. first + count - 1 from the vertices consecutive slices
-// share (their common band line): false when they share none.
-bool stripe_frame(const std::vector<double> &v, const std::vector<int32_t> &po, int first, int count, RowFrame &f) {
-    if (count < 2) return false;
-    double dx = 0, dy = 0;
-    std::vector<std::vector<std::pair<double, double>>> shared(count);
-    for (int k = 0; k + 1 < count; ++k) {
-        const int a0 = po[first + k], a1 = po[first + k + 1], b0 = po[first + k + 1], b1 = po[first + k + 2];
-        auto &sh = shared[k + 1];   // boundary between slices k and k + 1
-        for (int i = a0; i < a1; ++i)
-            for (int j = b0; j < b1; ++j)
-                if (std::fabs(v[2 * i] - v[2 * j]) < 1e-9 && std::fabs(v[2 * i + 1] - v[2 * j + 1]) < 1e-9) {
-                    sh.emplace_back(v[2 * i], v[2 * i + 1]);
-                    break;
-                }
-        if (sh.size() < 2) return false;
-        // the two shared points farthest apart give the boundary's direction
-        double best = -1, ex = 0, ey = 0;
-        for (auto &p : sh)
-            for (auto &q : sh) {
-                const double d = (p.first - q.first) * (p.first - q.first) + (p.second - q.second) * (p.second - q.second);
-                if (d > best) best = d, ex = q.first - p.first, ey = q.second - p.second;
-            }
-        if (dx * ex + dy * ey < 0) ex = -ex, ey = -ey;
-        const double n = std::sqrt(ex * ex + ey * ey);
-        dx += ex / n;
-        dy += ey / n;
-    }
-    const double n = std::sqrt(dx * dx + dy * dy);
-    if (!(n > 0)) return false;
-    f.nx = -dy / n;
-    f.ny = dx / n;
-    std::vector<double> b(count, 0.0);
-    for (int k = 1; k < count; ++k) {
-        for (auto &p : shared[k]) b[k] += p.first * f.nx + p.second * f.ny;
-        b[k] /= (double)shared[k].size();
-    }
-    if (count > 2 && b[count - 1] < b[1]) {
-        f.nx = -f.nx, f.ny = -f.ny;
-        for (int k = 1; k < count; ++k) b[k] = -b[k];
-    }
-    const double w = count > 2 ? (b[count - 1] - b[1]) / (count - 2) : 1.0;
-    if (!(w > 0)) return false;
-    f.b1 = b[1];
-    f.inv_h = 1.0 / w;
-    f.jmax = count - 2;
-    return true;
-}
-
-// The row-interval records of a 32-bit-cell scene (d_rows), or none (NULL) when the grid is too
-// wide for 16-bit column bounds, the slices share no band line, or a row / cell breaks the
-// interval or stripe-pair shape.
-wgrt_status build_rows(wgrt_scene *s) {
-    const LocatorHost &L = s->loc_host;
-    const int ncx = L.ncx, ncy = L.ncy;
-    if (!s->d_cells32 || ncx >= 0xffff || s->nfc < 2 || s->noc < 2) return WGRT_OK;
-    RowFrame ff{}, of{};
-    if (!stripe_frame(L.verts, L.poly_off, 3, s->nfc, ff) || !stripe_frame(L.verts, L.poly_off, 3 + s->nfc, s->noc, of))
-        return WGRT_OK;
-    const int chunks = 2 + (s->nfc - 1) + (s->noc - 1);
-    int *bad = nullptr;
-    HIP_TRY(hipMalloc((void **)&bad, sizeof(int)));
-    hipError_t e = hipMemset(bad, 0, sizeof(int));
-    if (e == hipSuccess) e = hipMalloc((void **)&s->d_rows, (size_t)ncy * chunks * sizeof(uint4));
-    if (e == hipSuccess) {
-        hipLaunchKernelGGL(row_bounds_kernel, dim3((unsigned)ncy), dim3(256), 0, 0, s->d_cells32, ncx, s->nfc, s->noc,
-                           chunks, s->d_rows, bad);
-        e = hipGetLastError();
-    }
-    if (e == hipSuccess) {
-        const int64_t n = (int64_t)ncx * ncy;
-        hipLaunchKernelGGL(cover_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, 0, s->d_cells32, ncx, ncy, L.x0,
-                           L.y0, L.h, s->nfc, s->noc, ff, of, bad);
-        e = hipGetLastError();
-    }
-    int hb = 0;
-    if (e == hipSuccess) e = hipMemcpy(&hb, bad, sizeof(int), hipMemcpyDeviceToHost);
-    (void)hipFree(bad);
-    if (e != hipSuccess || hb) {
-        (void)hipFree(s->d_rows);
-        s->d_rows = nullptr;
-    }
-    if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("row records: ") + hipGetErrorString(e));
-    s->row_chunks = chunks;
-    s->oc_chunk0 = 2 + (s->nfc - 1);
-    s->fc_frame = ff;
-    s->oc_frame = of;
-    return WGRT_OK;
-}
-
 extern "C" {
 
 wgrt_status wgrt_scene_create(const wgrt_scene_desc *desc, int device, wgrt_scene **out) {
@@ -1101,7 +914,6 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
         HIP_TRY(grid_of((const void *)trace_jones_tl_kernel<uint32_t, true, false>, s->jones_tl_grid[1]));
     }
     s->loc_host = host.loc;
-    if ((st = build_rows(s)) != WGRT_OK) return bail(st);
     s->loc_host.cells.clear();
     s->loc_host.cells.shrink_to_fit();
     s->loc_host.row_edges.clear();
@@ -1119,7 +931,6 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_jtiles);
     (void)hipFree(s->d_cells);
     (void)hipFree(s->d_cells32);
-    (void)hipFree(s->d_rows);
     (void)hipFree(s->d_verts);
     (void)hipFree(s->d_poly_off);
     (void)hipFree(s->d_row_off);
