@@ -1183,7 +1183,16 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     int64_t grid = c.workgroups > 0 ? c.workgroups
                    : timeline     ? s->jones_tl_grid[num_iter > 1]
                                   : s->jones_grid[variant == 9][num_iter > 1][single];
-    const int64_t useful = (n_rays + 255) / 256;
+    // a workgroup's 4 waves need 4 work items to all have work (debug chunk_rays: smaller items)
+    const int64_t item = (dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk;
+    const int64_t useful = (n_rays + 4 * item - 1) / (4 * item);
+    if (c.workgroups <= 0 && !timeline && num_iter <= 1) {
+        // a single trace of a small batch (C2: 1,936 items for 4,096 resident waves) is its rays'
+        // longest chains, which run faster on a less crowded chip: about two items per wave
+        // (C2 -11 %; batches of more than ~7,700 items keep the resident grid)
+        const int64_t want = (2 * ((n_rays + item - 1) / item) + 14) / 15;
+        if (grid > want) grid = want;
+    }
     if (grid > useful) grid = useful;
     wgrt_scene *ms = const_cast<wgrt_scene *>(s);
     wgrt_scene::Scratch *sc = nullptr;

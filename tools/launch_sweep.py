@@ -1,0 +1,60 @@
+#!/usr/bin/env python3
+"""Single-launch time over work-item size (wgrt_debug_opts.chunk_rays) and persistent-grid size
+(workgroups) for one bench config: does a small batch (C2: 0.12M rays, fewer 64-ray items than
+the 4,096 waves) trace faster with smaller items or fewer waves?  One process, HIP events, the
+median of --launches launches per point; one JSON line per point.
+
+  python tools/launch_sweep.py --config C2 --chunks 64 32 16 --workgroups 0 512 256"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--config", default="C2")
+    ap.add_argument("--chunks", type=int, nargs="+", default=[64, 32, 16])
+    ap.add_argument("--workgroups", type=int, nargs="+", default=[0, 512, 256])
+    ap.add_argument("--launches", type=int, default=10)
+    a = ap.parse_args()
+    import torch
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS, build_inputs
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import hip_shard_builder, make_shard
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, new_stats, trace_fullcolor
+    w = CONFIGS[a.config]
+    nx, ny, lam, R = w.nx, w.ny, list(w.lambdas), w.R
+    dev = torch.device("cuda", 0)
+    g, L, pts = build_inputs(w)
+    sc = Scene.from_geometry(g, L)
+    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(make_shard(nx, ny, len(lam), R, 1, 0))
+    eb = torch.zeros(sc.eb_shape(), dtype=torch.float32, device=dev)
+    st = new_stats(dev)
+    for wg in a.workgroups:
+        for ch in a.chunks:
+            dbg = dict(chunk_rays=ch) if ch != 64 else None
+            for _ in range(3):
+                trace_fullcolor(sc, rays, rng, eb, workgroups=wg, debug=dbg)
+            torch.cuda.synchronize()
+            st.zero_()
+            ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
+                  for _ in range(a.launches)]
+            for s, e in ev:
+                s.record()
+                trace_fullcolor(sc, rays, rng, eb, stats=st, workgroups=wg, debug=dbg)
+                e.record()
+            torch.cuda.synchronize()
+            ms = float(np.median([s.elapsed_time(e) for s, e in ev]))
+            b = int(st[0]) / a.launches
+            print(json.dumps({"config": a.config, "workgroups": wg, "chunk_rays": ch, "single_ms": round(ms, 4),
+                              "bounces_per_launch": b, "ray_bounces_per_s": round(b / ms * 1e3, 1)}), flush=True)
+    sc.close()
+
+
+if __name__ == "__main__":
+    main()
