@@ -21,6 +21,7 @@ def main():
     ap.add_argument("--chunks", type=int, nargs="+", default=[64, 32, 16])
     ap.add_argument("--workgroups", type=int, nargs="+", default=[0, 512, 256])
     ap.add_argument("--launches", type=int, default=10)
+    ap.add_argument("--num-iter", type=int, default=1, help="chained traces per call (fused launch when > 1)")
     a = ap.parse_args()
     import torch
 
@@ -39,20 +40,21 @@ def main():
         for ch in a.chunks:
             dbg = dict(chunk_rays=ch) if ch != 64 else None
             for _ in range(3):
-                trace_fullcolor(sc, rays, rng, eb, workgroups=wg, debug=dbg)
+                trace_fullcolor(sc, rays, rng, eb, workgroups=wg, debug=dbg, num_iter=a.num_iter)
             torch.cuda.synchronize()
             st.zero_()
             ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
                   for _ in range(a.launches)]
             for s, e in ev:
                 s.record()
-                trace_fullcolor(sc, rays, rng, eb, stats=st, workgroups=wg, debug=dbg)
+                trace_fullcolor(sc, rays, rng, eb, stats=st, workgroups=wg, debug=dbg, num_iter=a.num_iter)
                 e.record()
             torch.cuda.synchronize()
-            ms = float(np.median([s.elapsed_time(e) for s, e in ev]))
-            b = int(st[0]) / a.launches
-            print(json.dumps({"config": a.config, "workgroups": wg, "chunk_rays": ch, "single_ms": round(ms, 4),
-                              "bounces_per_launch": b, "ray_bounces_per_s": round(b / ms * 1e3, 1)}), flush=True)
+            ms = float(np.median([s.elapsed_time(e) for s, e in ev])) / a.num_iter
+            b = int(st[0]) / a.launches / a.num_iter
+            print(json.dumps({"config": a.config, "workgroups": wg, "chunk_rays": ch, "num_iter": a.num_iter,
+                              "ms_per_trace": round(ms, 4),
+                              "bounces_per_trace": b, "ray_bounces_per_s": round(b / ms * 1e3, 1)}), flush=True)
     sc.close()
 
 
