@@ -1187,10 +1187,17 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     const int64_t item = (dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk;
     const int64_t useful = (n_rays + 4 * item - 1) / (4 * item);
     if (c.workgroups <= 0 && !timeline && num_iter <= 1) {
-        // a single trace of a small batch (C2: 1,936 items for 4,096 resident waves) is its rays'
-        // longest chains, which run faster on a less crowded chip: about two items per wave
-        // (C2 -11 %; batches of more than ~7,700 items keep the resident grid)
-        const int64_t want = (2 * ((n_rays + item - 1) / item) + 14) / 15;
+        // a single trace ends with the drain of its longest ray chains, and chains run faster
+        // on a less crowded chip, while the bulk before it wants every resident wave: the grid
+        // that balances bulk throughput (work / W) against drain crowding (~ W) grows as
+        // sqrt(work items).  K = 6.5 workgroups per sqrt(item), measured: C2
+        // (1,936 items, 287 workgroups) -11 %, half and quarter C3 shards -8 / -12 %; C3 (946)
+        // unchanged; C4 and larger keep the resident grid
+#ifndef WGRT_GRID_SQRT_K
+#define WGRT_GRID_SQRT_K 6.5
+#endif
+        const int64_t items = (n_rays + item - 1) / item;
+        const int64_t want = (int64_t)std::ceil(WGRT_GRID_SQRT_K * std::sqrt((double)items));
         if (grid > want) grid = want;
     }
     if (grid > useful) grid = useful;
