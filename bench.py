@@ -9,27 +9,30 @@ One step = one trace of every ray of the batch = ONE launch of the reference's k
 (gpu_ray_tracing_pro_fullColor.py:169-177 issues num_iter = 4 of them, each starting from
 the RNG states the previous one left and adding its out-couplings to the eyebox grid).  The
 headline ``value`` times K such steps as K separate launches (``num_iter = 1`` each, SURVEY.md
-§8(d)), inputs already resident in HBM, plus the eyebox collective at N > 1.  Two more rates of
-the same batch ride along: ``main_job`` -- the reference's job shape, 4 chained traces issued as
-one call (the engine fuses them into one persistent launch, bit-identical to 4 launches) -- and
-``fused`` -- all K steps in one call.
+§8(d)), inputs already resident in HBM, plus the eyebox collective at N > 1.  More rates of the
+same batch ride along: ``main_job`` -- the reference's job shape, 4 chained traces issued as one
+call (the engine fuses them into one persistent launch, bit-identical to 4 launches) --,
+``fused`` -- all K steps in one call -- and ``long_region`` -- the headline's single launches
+over a timed region of at least LONG_STEPS steps (>= 50 ms; the driver's K = 20 gives a 5-ms region).
 
 Workloads (``--config``, BASELINE.json configs, configs.py):
     C2  single-lambda 532 nm, 11x11 FoV, num_rays_per_FoV = 1024
     C3  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 1024 (the metric's workload)
     C4  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 4096
     C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce stress
-    auto (default) = C3 at every N: every GPU traces the metric's workload.
+    auto (default) = C3: the metric's workload.
 Multi-GPU: one process per GPU through distributed.py.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
-``--scaling weak`` (default): every rank traces the whole C3 batch as its own replica (the same
-columns, global ray ids offset by rank x batch, so its own random streams: N ranks trace the
-reference kernel over the batch tiled N times), and one RCCL sum-reduce of the eyebox grid to
-rank 0 closes the timed region -- per-GPU work fixed, the north star's single eyebox reduce.
-``--scaling strong``: the one batch split over the ranks (interleaved FoV x wavelength blocks, the
-eyebox slabs gathered to rank 0 -- the reference-flow driver's sharding); a C3 batch split 8 ways
-is bound by its longest ray chains, not by the GPUs.  ``--emulate-ranks N`` times
-each of N strong-scaling shards in turn on one GPU and prints the predicted N-GPU step time.
+``--scaling strong`` (default): the metric's one batch split over the N ranks -- interleaved FoV x
+wavelength blocks (BASELINE config 4's "FoV x lambda sharded"), each rank's eyebox slabs gathered to
+rank 0 over RCCL -- so ``value`` is the batch's bounces over the slowest rank's time; at N = 8 a C3
+batch is bound by its longest ray chains, not by the GPUs.  At N > 1 the line also
+carries ``weak``: every rank tracing the whole batch as its own replica (global ray ids offset by
+rank x batch) with one RCCL sum-reduce of the grid -- weak scaling, reported beside the metric's
+curve, never as it.  ``--scaling weak`` makes the replicas the headline.  At N = 1 the line carries
+``emulated_strong``: each of the N = 2 / 4 / 8 strong-scaling shards of C3 and C4 traced alone on
+the one GPU (single launches, and the reference's 4-chained job per shard), i.e. the N-GPU step
+time the curve should show before the collective.  ``--emulate-ranks N`` prints one such record.
 """
 from __future__ import annotations
 
@@ -48,19 +51,22 @@ sys.path.insert(0, REPO)
 ALGO_BYTES_PER_BOUNCE = 72      # read + write of the minimal 36-B ray record
 HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 LIFETIME_BUCKETS = (1, 10, 30, 100, 300, 1000)   # bounce-count histogram edges (last bucket open)
+LONG_STEPS = 200                # long_region: >= 50 ms of C3 single launches
+EMULATE_STEPS = 20              # single launches per shard in the emulated_strong record
 
 
 def parse(argv=None):
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--steps", type=int, default=LONG_STEPS)
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--config", default="auto", choices=["auto", "C2", "C3", "C4", "C5"])
     ap.add_argument("--lut-seed", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
-    ap.add_argument("--scaling", default="weak", choices=["weak", "strong"],
-                    help="N > 1: weak = one replica of the batch per rank (global ids offset per rank), eyebox "
-                         "sum-reduce; strong = the batch split over the ranks")
+    ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],
+                    help="N > 1: strong = the metric's batch split over the ranks (FoV x lambda blocks, eyebox "
+                         "gather); weak = one replica of the batch per rank (global ids offset per rank), eyebox "
+                         "sum-reduce")
     ap.add_argument("--assign", default="interleaved", choices=["interleaved", "contiguous"],
                     help="FoV x wavelength blocks per rank (distributed.rank_blocks)")
     ap.add_argument("--collective", default="gather", choices=["gather", "reduce"],
@@ -68,7 +74,8 @@ def parse(argv=None):
                          "or sum-reduce the whole grid")
     ap.add_argument("--emulate-ranks", type=int, default=0, metavar="N",
                     help="one GPU: time each of N ranks' shards in turn (predicted N-GPU step time)")
-    ap.add_argument("--no-extras", action="store_true", help="skip the main_job / fused rates")
+    ap.add_argument("--no-extras", action="store_true",
+                    help="skip the main_job / fused / long_region / weak / emulated_strong records")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--dist-backend", default="nccl", choices=["nccl", "gloo"],
                     help="process-group backend for N > 1 (nccl = RCCL over xGMI; gloo only to rehearse the "
@@ -159,7 +166,9 @@ def main(argv=None):
     scene = Scene.from_geometry(geom, luts, device=local)
     t_scene = time.perf_counter() - t_scene
     if a.emulate_ranks:
-        emulate(a, cname, w, scene, points, dev)
+        rec = emulate_shards(scene, w, points, a.emulate_ranks, a.steps, a.warmup, dev, a.variant, a.assign)
+        print(json.dumps({"emulated_ranks": a.emulate_ranks, "config": f"{cname}: {w.name}", "assign": a.assign,
+                          **rec}), flush=True)
         scene.close()
         return
     weak = a.scaling == "weak"
@@ -176,27 +185,39 @@ def main(argv=None):
     else:
         collect = reduce_eyebox
 
-    def timed(steps, per_call, events=True):
+    def timed(steps, per_call, events=True, sh=None, r_=None, g_=None, coll=None):
         """steps chained traces as calls of per_call traces (distributed.timed_run: barrier, sync,
         trace, eyebox collective, sync, barrier; time MAX and bounces SUM over ranks); with events,
         HIP events around every call on the stream the kernels run on (torch's current stream)."""
         ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True))
               for _ in split_calls(steps, per_call)] if events else []
         hook = (lambda j, what: ev[j][0 if what == "start" else 1].record()) if events else None
-        elapsed, b_total, b_local = timed_run(tracer, rays, rng, eb, shard.gid, steps, per_call, stats,
-                                              sync=torch.cuda.synchronize, hook=hook, collect=collect)
+        elapsed, b_total, b_local = timed_run(tracer, r_ if r_ is not None else rays, g_ if g_ is not None else rng,
+                                              eb, (sh or shard).gid, steps, per_call, stats,
+                                              sync=torch.cuda.synchronize, hook=hook, collect=coll or collect)
         check_stats(stats)
         return elapsed, b_total, b_local, [s.elapsed_time(e) for s, e in ev]
 
     # warm-up: W separate launches (and one fused call, so the fused kernels are loaded too); the
-    # first one records the per-ray lifetimes of a trace
+    # first one records the per-ray lifetimes and the bounce kinds of a trace
     per_ray = torch.zeros(shard.n_rays, dtype=torch.int32, device=dev)
+    kinds = None
     if shard.n_rays:
         g = shard.gid
         kw = dict(gid_offset=g.offset) if g.offset is not None else dict(
             gid_blocks=torch.as_tensor(g.block_gid, device=dev), gid_block_rays=R)
-        trace_fullcolor(scene, rays, rng, eb, per_ray_bounces=per_ray, variant=a.variant, **kw)
+        st0 = new_stats(dev)
+        trace_fullcolor(scene, rays, rng, eb, per_ray_bounces=per_ray, variant=a.variant, stats=st0, **kw)
+        s0 = [int(v) for v in st0.cpu()]
+        traced = shard.n_rays - s0[1]
+        kinds = {"in_coupling": traced, "interactions": s0[5], "hops_switches_exits": s0[0] - traced - s0[5],
+                 "note": "one trace's bounces by kind (wgrt_trace_stats): the in-coupling event of every ray "
+                         "(GRTF:860-904), the loop iterations with a Monte-Carlo draw (coupler interactions), and "
+                         "the iterations without one (miss hops, R3->R4 switches, terminations at GRTF:906 / "
+                         "1244-1246)"}
     lifetimes = lifetime_histogram(per_ray)
+    if kinds is not None:
+        lifetimes["kinds"] = kinds
     run_steps(tracer, rays, rng, eb, shard.gid, max(a.warmup - 1, 0), 1)
     if not a.no_extras:
         run_steps(tracer, rays, rng, eb, shard.gid, 2, 0)
@@ -219,34 +240,72 @@ def main(argv=None):
             e_el, e_b, e_bl, e_ms = timed(steps, 0)
             extras[key] = {"value": round(e_b / e_el, 1), "ms_per_step": round(e_el / steps * 1e3, 4),
                            "steps": steps, "kernel_avg_ms": round(float(np.mean(e_ms)), 4), "note": note}
+        if a.steps < LONG_STEPS:
+            l_el, l_b, _, _ = timed(LONG_STEPS, 1, events=False)
+            extras["long_region"] = {
+                "value": round(l_b / l_el, 1), "ms_per_step": round(l_el / LONG_STEPS * 1e3, 4), "steps": LONG_STEPS,
+                "timed_region_s": round(l_el, 4),
+                "note": f"the headline's single launches timed over {LONG_STEPS} steps (the K-step region is "
+                        f"{elapsed * 1e3:.1f} ms)"}
+        if world > 1 and not weak:
+            # weak scaling beside the metric's curve: every rank traces a replica of the whole batch
+            wshard = replica_shard(nx, ny, len(lambdas), R, world, rank)
+            wr, wg = hip_shard_builder(points, nx, ny, lambdas, R, dev)(wshard)
+            reserve(scene, wshard.n_rays, 1)
+            run_steps(tracer, wr, wg, eb, wshard.gid, 2, 1)
+            reduce_eyebox(eb, None)
+            w_el, w_b, _, _ = timed(a.steps, 1, events=False, sh=wshard, r_=wr, g_=wg, coll=reduce_eyebox)
+            extras["weak"] = {
+                "value": round(w_b / w_el, 1), "ms_per_step": round(w_el / a.steps * 1e3, 4), "steps": a.steps,
+                "rays_total": w.n_rays * world, "scaling": "weak",
+                "note": f"replicas: each of the {world} ranks traces the whole batch with its own global ray ids "
+                        "(the batch tiled N times), one RCCL sum-reduce of the eyebox grid; per-GPU work fixed -- "
+                        "not the metric's curve"}
+            del wr, wg
+    emulated = None
+    if world == 1 and not a.no_extras and cname == "C3":
+        emulated = emulated_strong(a, scene, dev, elapsed / a.steps * 1e3,
+                                   extras.get("main_job", {}).get("ms_per_step"))
 
     if rank == 0:
         kavg_s = float(np.mean(call_ms)) / 1e3
-        achieved = ev_bounces_local / len(call_ms) * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
+        bpl = ev_bounces_local / len(call_ms)
+        achieved = bpl * ALGO_BYTES_PER_BOUNCE / kavg_s / 1e9
         sha = lib_sha16()
-        traffic, traffic_note = None, "no PMC pass recorded for this library build"
+        traffic, traffic_raw, measured, traffic_note = None, None, None, "no PMC pass recorded for this library build"
         try:
             with open(a.traffic_json) as f:
                 ent = json.load(f).get(f"{cname}:v{a.variant}")
             if ent and ent.get("lib_sha16") == sha:
-                traffic = int(round(ent["bytes_per_bounce"] * ev_bounces_local / len(call_ms)))
-                traffic_note = ("rocprofv3 FETCH_SIZE + WRITE_SIZE of the trace kernel on this build (L2 <-> fabric "
-                                "bytes; Infinity-Cache hits included, so an upper bound on HBM bytes), per launch")
+                # MI355X_MICROARCH.md (HBM): on gfx950 FETCH_SIZE reports half the bytes of a read, so the
+                # corrected fabric traffic is 2 x FETCH_SIZE + WRITE_SIZE; scaled to this launch's bounces
+                scale = bpl / ent["bounces_per_launch"]
+                traffic_raw = int(round((ent["fetch_bytes_per_launch"] + ent["write_bytes_per_launch"]) * scale))
+                traffic = int(round((2 * ent["fetch_bytes_per_launch"] + ent["write_bytes_per_launch"]) * scale))
+                measured = round(traffic / kavg_s / 1e9, 3)
+                traffic_note = ("rocprofv3 PMC passes of the trace kernel on this build (tools/pmc_traffic.py): traffic "
+                                "= 2 x FETCH_SIZE + WRITE_SIZE per launch (the guide's gfx950 correction of FETCH_SIZE; "
+                                "L2 <-> fabric bytes, Infinity-Cache hits included, so an upper bound on HBM bytes), "
+                                "traffic_raw = FETCH_SIZE + WRITE_SIZE; measured_gbps = traffic / launch_avg_ms")
         except (OSError, ValueError, KeyError):
             pass
         valu = pmc_roofline(a.pmc_json, f"{cname}:v{a.variant}", sha)
         roofline = {"bound": "hbm", "achieved": round(achieved, 3), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                    "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_note": traffic_note,
+                    "frac": round(achieved / HBM_PEAK_GBPS, 6), "traffic": traffic, "traffic_raw": traffic_raw,
+                    "measured_gbps": measured,
+                    "measured_frac": round(measured / HBM_PEAK_GBPS, 6) if measured is not None else None,
+                    "traffic_note": traffic_note,
                     "kernel": kernel_name(a.variant, scene), "launch_avg_ms": round(kavg_s * 1e3, 4),
                     "evented_ms_per_step": round(_el / a.steps * 1e3, 4),
                     "algo_bytes_per_bounce": ALGO_BYTES_PER_BOUNCE,
-                    "bounces_per_launch": int(round(ev_bounces_local / len(call_ms))),
+                    "bounces_per_launch": int(round(bpl)),
                     "valu": valu if valu is not None else {
                         "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
-                    "note": "launch_avg_ms: HIP events around each launch (trace kernel + its eyebox/replay "
-                            "epilogue kernel) on rank 0, in a second pass of the same K launches (the timed steps "
-                            "carry no event records); valu: the issue-side bound SURVEY.md §8(d) calls binding "
-                            "(VALU busy = SQ_ACTIVE_INST_VALU x 4 / (GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
+                    "note": "achieved = algorithmic bytes (72 B x bounces) / launch_avg_ms; launch_avg_ms: HIP events "
+                            "around each launch (trace kernel + its eyebox/replay epilogue kernel) on rank 0, in a "
+                            "second pass of the same K launches (the timed steps carry no event records); valu: the "
+                            "issue-side bound SURVEY.md §8(d) calls binding (VALU busy = SQ_ACTIVE_INST_VALU x 4 / "
+                            "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
         cpu = None
         if world == 1 and not a.no_cpu_baseline:
             cpu = cpu_baseline(geom, luts, points, nx, ny, lambdas, R, a.cpu_seconds)
@@ -271,6 +330,9 @@ def main(argv=None):
             "roofline": roofline,
             "main_job": extras.get("main_job"),
             "fused": extras.get("fused"),
+            "long_region": extras.get("long_region"),
+            "weak": extras.get("weak"),
+            "emulated_strong": emulated,
             "cpu_baseline": cpu,
         }
         print(json.dumps(line), flush=True)
@@ -279,46 +341,88 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
-def emulate(a, cname, w, scene, points, dev):
-    """--emulate-ranks N: each rank's shard traced alone on this GPU, K single launches each;
-    prints one JSON line with the per-rank ms per step and the predicted N-GPU step time (their
-    maximum; the eyebox collective is not included)."""
+def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="interleaved"):
+    """Each of the N strong-scaling shards of workload w (distributed.make_shard) traced alone on this
+    GPU: ``steps`` single launches (HIP events around them) and one 4-chained call (the reference's
+    job shape, MAIN:169-177, one persistent launch).  Returns the per-rank ms per step and the
+    predicted N-GPU step time = the slowest shard's (the eyebox collective not included)."""
     import torch
 
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
                                                                                 make_shard, run_steps)
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import check_stats, new_stats, reserve
-    N = a.emulate_ranks
     nx, ny, lambdas, R = w.nx, w.ny, list(w.lambdas), w.R
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     stats = new_stats(dev)
-    tracer = hip_tracer(scene, a.variant, stats)
+    tracer = hip_tracer(scene, variant, stats)
     per_rank = []
-    for r in range(N):
-        shard = make_shard(nx, ny, len(lambdas), R, N, r, a.assign)
-        rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard)
-        reserve(scene, shard.n_rays, 1)
-        run_steps(tracer, rays, rng, eb, shard.gid, a.warmup, 1)
-        torch.cuda.synchronize()
-        stats.zero_()
+
+    def ev_time(fn):
         t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         t0.record()
-        run_steps(tracer, rays, rng, eb, shard.gid, a.steps, 1)
+        fn()
         t1.record()
         torch.cuda.synchronize()
+        return t0.elapsed_time(t1)
+
+    for r in range(N):
+        shard = make_shard(nx, ny, len(lambdas), R, N, r, assign)
+        rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard)
+        reserve(scene, shard.n_rays, 4)
+        run_steps(tracer, rays, rng, eb, shard.gid, warmup, 1)
+        run_steps(tracer, rays, rng, eb, shard.gid, 4, 0)
+        torch.cuda.synchronize()
+        stats.zero_()
+        ms = ev_time(lambda: run_steps(tracer, rays, rng, eb, shard.gid, steps, 1)) / steps
         check_stats(stats)
-        ms = t0.elapsed_time(t1) / a.steps
+        b = int(stats[0].item()) // steps
+        job = ev_time(lambda: run_steps(tracer, rays, rng, eb, shard.gid, 4, 0)) / 4
+        check_stats(stats)
         per_rank.append({"rank": r, "rays": shard.n_rays, "ms_per_step": round(ms, 4),
-                         "bounces_per_step": int(stats[0].item()) // a.steps})
+                         "job_ms_per_step": round(job, 4), "bounces_per_step": b})
         del rays, rng
     worst = max(p["ms_per_step"] for p in per_rank)
+    worst_job = max(p["job_ms_per_step"] for p in per_rank)
     total = sum(p["bounces_per_step"] for p in per_rank)
-    print(json.dumps({"emulated_ranks": N, "config": f"{cname}: {w.name}", "assign": a.assign,
-                      "steps": a.steps, "per_rank": per_rank,
-                      "predicted_ms_per_step": worst,
-                      "predicted_value": round(total / (worst / 1e3), 1),
-                      "note": "each rank's shard timed alone on one MI355X; predicted N-GPU step = max over ranks, "
-                              "without the eyebox collective"}), flush=True)
+    return {"steps": steps, "per_rank": per_rank, "predicted_ms_per_step": worst,
+            "predicted_value": round(total / (worst / 1e3), 1), "predicted_job_ms_per_step": worst_job,
+            "predicted_job_value": round(total / (worst_job / 1e3), 1),
+            "note": "each rank's shard timed alone on one MI355X; predicted N-GPU step = max over ranks, "
+                    "without the eyebox collective"}
+
+
+def emulated_strong(a, scene, dev, ms_one, job_ms_one):
+    """The N = 2 / 4 / 8 strong-scaling curve of C3 (this scene) and C4 predicted on one GPU
+    (emulate_shards): per N the slowest shard's ms per step and the speedup over one GPU, for single
+    launches and for the reference's 4-chained job."""
+    import torch
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS, build_inputs
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene
+    steps = min(a.steps, EMULATE_STEPS)
+    out = {}
+    for cname in ("C3", "C4"):
+        w = CONFIGS[cname]
+        geom, luts, points = build_inputs(w, lut_seed=a.lut_seed)
+        sc = scene if cname == "C3" else Scene.from_geometry(geom, luts, device=dev.index or 0)
+        one, one_job = ms_one, job_ms_one
+        if cname != "C3":   # C4 on one GPU: the same measurement as the shards'
+            whole = emulate_shards(sc, w, points, 1, steps, 2, dev, a.variant, a.assign)
+            one, one_job = whole["predicted_ms_per_step"], whole["predicted_job_ms_per_step"]
+        rec = {"one_gpu_ms_per_step": round(one, 4), "one_gpu_job_ms_per_step": one_job}
+        for n in (2, 4, 8):
+            e = emulate_shards(sc, w, points, n, steps, 2, dev, a.variant, a.assign)
+            rec[str(n)] = {"ms_per_step": e["predicted_ms_per_step"], "speedup": round(one / e["predicted_ms_per_step"], 3),
+                           "value": e["predicted_value"], "job_ms_per_step": e["predicted_job_ms_per_step"],
+                           "job_speedup": (round(one_job / e["predicted_job_ms_per_step"], 3) if one_job else None)}
+        if sc is not scene:
+            sc.close()
+        out[cname] = rec
+        torch.cuda.synchronize()
+    out["note"] = ("strong scaling predicted on one MI355X: each of the N interleaved FoV x lambda shards "
+                   "(bench.py --gpus N --scaling strong) traced alone, the slowest one's step time; single "
+                   "launches and the reference's 4-chained job per shard; without the eyebox gather")
+    return out
 
 
 def kernel_name(variant, scene):

@@ -77,7 +77,26 @@ struct TraceArgs {
     // global ray ids of an interleaved shard (wgrt_launch_opts.gid_blocks): NULL = gid_offset + i
     const int64_t *gid_blocks;
     int64_t gid_block_rays;
+    // hop runs of the Jones-vector variants (wgrt_scene_opts.coarse_shift; coarse_shift 0 = off): the
+    // coarse locator's byte table (coarse_words 32-bit words, staged into LDS by every workgroup) and
+    // its palette of cell words
+    const uint32_t *coarse;
+    const uint64_t *coarse_pal;
+    int coarse_shift, coarse_nx, coarse_words;
 };
+
+// The coarse locator of the hop runs.  A block of 2^shift x 2^shift locator cells gets one byte:
+// kCoarseMixed when its cells do not all hold one cell word without an EDGE class, else that
+// word's palette index (bits 0-4) and, in bit 3 + R for R = 2, 3, 4, whether a miss hop of region
+// R continues at any point of the block (eff_reg1 IN, none of the region's slices IN, and for R3
+// eff_reg2 IN: advance() below then hops again).  The cells' IN / OUT classes are exact for every
+// point of their cell (wgrt_scene_build.cpp), so a uniform block's word is exact for every point of
+// the block, and a block index derived from a point's cell index (cell >> shift) is consistent with
+// the cell lookup by construction.
+constexpr int kCoarseMaxBytes = 18432;   // LDS budget of the byte table (per workgroup)
+constexpr int kCoarsePal = 31;           // palette entries (index 31 unused: 0xff stays free)
+constexpr uint32_t kCoarseMixed = 0xffu;
+constexpr int kPartWords = 8;            // counter partial slot of a trace workgroup (64-bit words)
 
 // A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
 // used (a volatile scalar load, a scalar-cache hit) instead of being held in an SGPR for the
@@ -957,65 +976,108 @@ __device__ __forceinline__ typename Loc::Word resolve_edges(const Loc &loc, type
 __device__ __forceinline__ int low_bit(uint32_t v) { return __builtin_ctz(v); }
 __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); }
 
-// Same contract as advance() for the Jones-vector lane: one loop iteration of GRTF:905-1246 that
-// needs no Monte-Carlo interaction (a miss hop or the R3 -> R4 switch: kTransit), or the next
-// interaction's block index, or kDie.  It tests the cell word loaded a pass earlier (JLane::pf);
-// a miss hop issues the load of the next one.  The outcome is computed as selects from the cell
-// word's class bits (in the word's own width: 32 bits for variant 7) -- one straight-line
+// The coarse locator's byte table and palette as staged in a workgroup's LDS (jones_body); shift 0:
+// no hop runs.
+typedef uint8_t __attribute__((address_space(3))) LdsU8;
+typedef uint64_t __attribute__((address_space(3))) LdsU64;
+struct CoarseLds {
+    const LdsU8 *b;
+    const LdsU64 *pal;
+    int shift, nx;
+};
+
+// Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246 that
+// need no Monte-Carlo interaction -- miss hops and the R3 -> R4 switch -- up to the next
+// interaction's block index (returned), a termination (kDie), or a position whose cell word must
+// come from the global locator (kTransit: its load is issued here, read by the next pass).  It
+// starts from the cell word loaded a pass earlier (JLane::pf).  The outcome is computed as selects
+// from the word's class bits (in the word's own width: 32 bits for variant 7) -- one straight-line
 // evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
-template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+//
+// Hop runs (C.shift > 0): a miss hop that lands in a uniform block of the coarse
+// locator knows its new cell word without a memory access -- the block's byte says whether the
+// region's miss hop continues there, and its palette word is the cell word -- so the lane keeps
+// hopping (each hop one bounce, the same float64 additions as one hop per pass) and evaluates the
+// word it lands on in the same pass; an R3 -> R4 switch is evaluated on, at the same position, too.
+// Only a landing in a mixed block ends the pass with a global cell-word load.
+#ifndef WGRT_HOP_MAX
+#define WGRT_HOP_MAX 1000000
+#endif
+template <bool RUNS, class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, const CoarseLds &C, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
     constexpr W kTop = (W)1 << (kBits - 1);
     JRay &r = L.r;
     W c = (W)L.pf;
-    const int region = r.region;
     const int nfc = A.nfc, noc = A.noc;
-    // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
-    const bool fc = region <= 3;
-    const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
-    const W gmask = 2 * count < kBits ? ((W)1 << (2 * count)) - (W)1 : (W)~(W)0;
-    W f = (c >> (2 * first)) & gmask;
-    W in = f & kLow, cand = in | ((f >> 1) & kLow);
-    const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
-    const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
-    const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
-    if (e1edge | sedge | e2edge) {
-        c = resolve_edges(loc, c, region, first, count, r.x, r.y);
-        f = (c >> (2 * first)) & gmask;
-        in = f & kLow;
-        cand = in | ((f >> 1) & kLow);
+    for (;;) {
+        const int region = r.region;
+        // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
+        const bool fc = region <= 3;
+        const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
+        const W gmask = 2 * count < kBits ? ((W)1 << (2 * count)) - (W)1 : (W)~(W)0;
+        W f = (c >> (2 * first)) & gmask;
+        W in = f & kLow, cand = in | ((f >> 1) & kLow);
+        const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
+        const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
+        const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
+        if (e1edge | sedge | e2edge) {   // never for a palette word (no EDGE class)
+            c = resolve_edges(loc, c, region, first, count, r.x, r.y);
+            f = (c >> (2 * first)) & gmask;
+            in = f & kLow;
+            cand = in | ((f >> 1) & kLow);
+        }
+        const bool over = L.bounces > (uint32_t)kMaxLoop;   // range(1e5) exhausted (GRTF:905)
+        const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
+        const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
+        const bool ic = region <= 1;
+        const bool hit = !ic & (cand != 0);
+        const int sl = low_bit((W)(cand | kTop)) >> 1;
+        const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
+        const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
+        const bool hop = !die & !ic & !hit & !sw;                               // miss hop
+        const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
+        L.bounces += over ? 0u : 1u;
+        kind = ic ? 0 : region - 1;
+        r.region = sw ? 4 : region;
+        if (!hop) {
+            // the switch keeps the position and its cell word: with hop runs, evaluate R4 on it now
+            if (RUNS && (sw & (C.shift > 0))) continue;
+            return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
+        }
+        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178); delta_phase += 2 lut_TIR (GRTF:1052,
+        // 1108, 1178) as a turn of Etm at the hop itself: a deferred per-interaction loop ran
+        // max(hops) iterations over a wave's lanes (+3 % single launch, +5 % fused on C3)
+        uint32_t b = kCoarseMixed;
+        int ix, iy;
+        for (int hops = 0;; ++hops) {
+            r.x = r.x + r.gx;
+            r.y = r.y + r.gy;
+            const double mr = r.mr;
+            r.mr = fma(mr, r.hr, -r.mi * r.hi);
+            r.mi = fma(mr, r.hi, r.mi * r.hr);
+            // the landing cell (locate_c's clamped index: the grid has a border of all-OUT cells)
+            ix = min(max((int)((r.x - loc.x0) * loc.inv_h), 0), loc.ncx - 1);
+            iy = min(max((int)((r.y - loc.y0) * loc.inv_h), 0), loc.ncy - 1);
+            if (!RUNS || C.shift == 0) break;
+            b = C.b[(iy >> C.shift) * C.nx + (ix >> C.shift)];
+            if (hops >= WGRT_HOP_MAX) break;
+            // the region's miss hop continues in this block (bit 3 + region; never in a mixed block,
+            // and the loop cap is the evaluation's own test)
+            if (!(((b >> (3 + region)) & 1u) & (b != kCoarseMixed) & (L.bounces <= (uint32_t)kMaxLoop))) break;
+            ++L.bounces;
+        }
+        if (b == kCoarseMixed) {
+            L.pf = loc.cells[iy * loc.ncx + ix];   // read by the next pass
+            return kTransit;
+        }
+        c = (W)C.pal[b & 31u];
+        L.pf = c;
     }
-    const bool over = L.bounces > (uint32_t)kMaxLoop;   // range(1e5) exhausted (GRTF:905)
-    const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
-    const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
-    const bool ic = region <= 1;
-    const bool hit = !ic & (cand != 0);
-    const int sl = low_bit((W)(cand | kTop)) >> 1;
-    const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
-    const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
-    const bool hop = !die & !ic & !hit & !sw;                               // miss hop
-    const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
-    L.bounces += over ? 0u : 1u;
-    kind = ic ? 0 : region - 1;
-    r.region = sw ? 4 : region;
-    if (hop) {
-        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178)
-        r.x = r.x + r.gx;
-        r.y = r.y + r.gy;
-        // delta_phase += 2 lut_TIR (GRTF:1052, 1108, 1178) as a turn of Etm at the hop itself: a
-        // deferred per-interaction loop ran max(hops) iterations over a wave's lanes (+3 % single
-        // launch, +5 % fused on C3, +10 % on C5's short hops)
-        const double mr = r.mr;
-        r.mr = fma(mr, r.hr, -r.mi * r.hi);
-        r.mi = fma(mr, r.hi, r.mi * r.hr);
-        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
-    }
-    return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
 }
 
 template <class LaneT>
@@ -1031,11 +1093,13 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 
 // Per-wave reduction of the ray counters, then one 64-bit atomic per counter per wave.
 __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t bounces, uint64_t hits,
-                                          uint64_t bad) {
+                                          uint64_t bad, uint64_t inter) {
     bounces = wave_sum(bounces);
     hits = wave_sum(hits);
     bad = wave_sum(bad);
+    inter = wave_sum(inter);
     if ((threadIdx.x & 63) == 0 && stats) {
+        if (inter) atomicAdd((unsigned long long *)&stats->interactions, (unsigned long long)inter);
         if (bounces) atomicAdd((unsigned long long *)&stats->bounces, (unsigned long long)bounces);
         if (hits) atomicAdd((unsigned long long *)&stats->eyebox_hits, (unsigned long long)hits);
         if (bad) atomicAdd((unsigned long long *)&stats->bad_rays, (unsigned long long)bad);
@@ -1044,9 +1108,9 @@ __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t boun
 
 // Trace ray i to termination with the reference arithmetic (variant 1's lane; replays).  With
 // s_io, the trace starts from *s_io instead of rng_states[i] and leaves its final state there
-// (rng_states untouched).
+// (rng_states untouched).  ni (optional) counts the interactions after the in-coupling event.
 __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad,
-                                          uint32_t *s_io = nullptr) {
+                                          uint32_t *s_io = nullptr, uint64_t *ni = nullptr) {
     Lane L;
     if (!lane_load(A, i, L)) {
         ++bad;
@@ -1062,6 +1126,7 @@ __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_
         entry = false;
         blk = advance(A, A.loc, L, kind);
         if (blk < 0) break;
+        if (ni) ++*ni;
     }
     if (s_io) *s_io = L.r.s;
     else lane_retire(A, L);

@@ -67,9 +67,9 @@ constexpr double kDefaultCellMm = WGRT_CELL_MM;
 // Variant 1: one ray per lane over a 1-D grid (the reference's launch shape, MAIN:167).
 __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t b = 0, h = 0, bad = 0;
-    if (i < A.n_rays) trace_one(A, i, b, h, bad);
-    add_stats(A.stats, b, h, bad);
+    uint64_t b = 0, h = 0, bad = 0, ni = 0;
+    if (i < A.n_rays) trace_one(A, i, b, h, bad, nullptr, &ni);
+    add_stats(A.stats, b, h, bad, ni);
 }
 
 // Launch scratch counters of the Jones-vector variants: kHeads work-queue heads, then the replay
@@ -96,11 +96,11 @@ constexpr int kQBlock = WGRT_QBLOCK;    // out-coupling queue slots a wave reser
                                // out-couples ~10 rays per trace)
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
-    __shared__ unsigned long long red[4][4];
+    __shared__ unsigned long long red[4][5];
     const unsigned long long nr = *A.replay_count, nf = *A.full_count;
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
-    uint64_t h = 0, b = 0, bad = 0, gu = 0;
+    uint64_t h = 0, b = 0, bad = 0, gu = 0, ni = 0;
     for (unsigned long long e = tid; e < nf * kQBlock; e += nth) {
         {
             const unsigned long long j = (unsigned long long)A.full_list[e / kQBlock] * kQBlock + e % kQBlock;
@@ -114,21 +114,22 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     for (unsigned long long k = tid; k < nr; k += nth) {
         const int64_t i = (int64_t)A.replay_list[k];
         if (A.n_iter <= 1) {
-            trace_one(A, i, b, h, bad);
+            trace_one(A, i, b, h, bad, nullptr, &ni);
         } else {   // fused launch: the traces from the abandoned one to the last, chained
             const uint64_t w = A.rng64[i];
             uint32_t st = (uint32_t)(w >> 32);
-            for (int it = (int)(w & 0xffu); it < A.n_iter; ++it) trace_one(A, i, b, h, bad, &st);
+            for (int it = (int)(w & 0xffu); it < A.n_iter; ++it) trace_one(A, i, b, h, bad, &st, &ni);
             A.rng[i] = st;
         }
     }
     if (blockIdx.x == 0) {
         for (int k = threadIdx.x; k < A.n_trace_waves; k += blockDim.x) {
-            const unsigned long long *slot = A.part + 4 * (size_t)k;
+            const unsigned long long *slot = A.part + kPartWords * (size_t)k;
             b += slot[0];
             bad += slot[1];
             h += slot[2];
             gu += slot[3];
+            ni += slot[4];
         }
         if (threadIdx.x < kScratchCtr) A.other_ctr[threadIdx.x] = 0ull;
     }
@@ -137,11 +138,13 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     bad = wave_sum(bad);
     h = wave_sum(h);
     gu = wave_sum(gu);
+    ni = wave_sum(ni);
     if ((threadIdx.x & 63) == 0) {
         red[w][0] = b;
         red[w][1] = bad;
         red[w][2] = h;
         red[w][3] = gu;
+        red[w][4] = ni;
     }
     __syncthreads();
     if (threadIdx.x == 0 && A.stats) {
@@ -150,6 +153,8 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
         const unsigned long long t1 = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
         const unsigned long long t3 = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+        const unsigned long long t4 = red[0][4] + red[1][4] + red[2][4] + red[3][4];
+        if (t4) atomicAdd((unsigned long long *)&st->interactions, t4);
         if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
         if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
         if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
@@ -219,6 +224,17 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
+    // the coarse locator of the hop runs, staged into this workgroup's LDS (every wave of the
+    // workgroup takes part, before any of them starts its loop)
+    __shared__ uint32_t coarse_lds[kCoarseMaxBytes / 4];
+    __shared__ uint64_t coarse_pal[32];
+    CoarseLds C{(const LdsU8 *)(LdsU32 *)coarse_lds, (const LdsU64 *)coarse_pal, A.coarse_shift, A.coarse_nx};
+    if (A.coarse_shift > 0) {
+        const uint32_t *const src = KA(coarse);
+        for (int k = threadIdx.x; k < A.coarse_words; k += blockDim.x) coarse_lds[k] = src[k];
+        if (threadIdx.x < 32) coarse_pal[threadIdx.x] = KA(coarse_pal)[threadIdx.x];
+        __syncthreads();
+    }
     int head = xcc_id();
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
     // debug timeline (TL instantiations only): per wave, start / queue exhausted / end
@@ -237,7 +253,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     bool entry = false;
     // per-lane totals in 32 bits: a lane's bounce total is added to the stats directly before it
     // could overflow (2^31 bounces on one lane: never in practice)
-    uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0;
+    uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0, tot_int = 0;
     unsigned long long wait_t0 = 0;    // fused: when this lane started waiting for its ray (s_memrealtime)
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
@@ -337,6 +353,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         bool out = false;
         if (active && blk >= 0) {
+            tot_int += entry ? 0u : 1u;
             const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
@@ -381,9 +398,15 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
     };
 
+#ifndef WGRT_HOP_BULK
+#define WGRT_HOP_BULK 1
+#endif
+#ifndef WGRT_HOP_TAIL
+#define WGRT_HOP_TAIL 1
+#endif
     for (;;) {
         if (active) {
-            blk = advance(A, loc, L, kind);
+            blk = advance<WGRT_HOP_BULK != 0>(A, loc, C, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
@@ -498,7 +521,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // The first pass continues the one the main loop broke off (advance and refill done).
         for (bool first = true;; first = false) {
             if (!first && active) {
-                blk = advance(A, loc, L, kind);
+                blk = advance<WGRT_HOP_TAIL != 0>(A, loc, C, L, kind);
                 entry = false;
                 if (blk == kDie) retire();
             }
@@ -529,24 +552,27 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
     }
     // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
-    __shared__ unsigned long long red[4][4];
+    __shared__ unsigned long long red[4][5];
     const uint64_t sum_b = wave_sum((uint64_t)tot_b);
     const uint64_t sum_bad = wave_sum((uint64_t)tot_bad);
     const uint64_t sum_h = wave_sum((uint64_t)tot_h);
     const uint64_t sum_g = FUSED ? wave_sum((uint64_t)tot_giveup) : 0ull;
+    const uint64_t sum_i = wave_sum((uint64_t)tot_int);
     if (lane == 0) {
         red[threadIdx.x >> 6][0] = sum_b;
         red[threadIdx.x >> 6][1] = sum_bad;
         red[threadIdx.x >> 6][2] = sum_h;
         red[threadIdx.x >> 6][3] = sum_g;
+        red[threadIdx.x >> 6][4] = sum_i;
     }
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long *slot = KA(part) + 4 * (size_t)blockIdx.x;
+        unsigned long long *slot = KA(part) + kPartWords * (size_t)blockIdx.x;
         slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
         slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
         slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
         slot[3] = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+        slot[4] = red[0][4] + red[1][4] + red[2][4] + red[3][4];
     }
 }
 
@@ -711,6 +737,24 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *verts
     }
     edges = wave_sum(edges);
     if ((threadIdx.x & 63) == 0 && edges) atomicAdd(edge_cells, (unsigned long long)edges);
+}
+
+// The coarse locator of the hop runs: one thread per block of 2^shift x 2^shift cells -- the block's
+// first cell word, and whether every cell of the block holds it and it has no EDGE class (the
+// host build's coarse_reduce_host rule).
+__global__ __launch_bounds__(256) void coarse_blocks_kernel(const uint64_t *cells, int ncx, int ncy, int shift, int nbx,
+                                                            int nby, uint64_t *word, uint8_t *uniform) {
+    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (k >= (int64_t)nbx * nby) return;
+    const int bx = (int)(k % nbx), by = (int)(k / nbx);
+    const int x0 = bx << shift, y0 = by << shift;
+    const int x1 = min(x0 + (1 << shift), ncx), y1 = min(y0 + (1 << shift), ncy);
+    const uint64_t w0 = cells[(size_t)y0 * ncx + x0];
+    bool u = !coarse_has_edge(w0);
+    for (int y = y0; y < y1 && u; ++y)
+        for (int x = x0; x < x1 && u; ++x) u = cells[(size_t)y * ncx + x] == w0;
+    word[k] = w0;
+    uniform[k] = u ? 1 : 0;
 }
 
 // One thread per (lambda, m, n) tile: the exact lane's tile and its Jones-vector tile
@@ -890,6 +934,50 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
         s->edge_cells = (int64_t)ec;
     }
     {
+        // the coarse locator of the hop runs (from the cell words on the device, or the host's)
+        const LocatorHost &L = host.loc;
+        const int shift = coarse_shift_for(opts ? opts->coarse_shift : 0, L.ncx, L.ncy);
+        if (shift > 0) {
+            const int nbx = ((L.ncx - 1) >> shift) + 1, nby = ((L.ncy - 1) >> shift) + 1;
+            const size_t nb = (size_t)nbx * nby;
+            std::vector<uint64_t> word;
+            std::vector<uint8_t> uni;
+            if (host_build) {
+                coarse_reduce_host(L.cells, L.ncx, L.ncy, shift, word, uni);
+            } else {
+                uint64_t *dw = nullptr;
+                uint8_t *du = nullptr;
+                if ((st = alloc_n(nb, &dw)) != WGRT_OK || (st = alloc_n(nb, &du)) != WGRT_OK) {
+                    (void)hipFree(dw);
+                    return bail(st);
+                }
+                hipLaunchKernelGGL(coarse_blocks_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, 0,
+                                   s->d_cells, L.ncx, L.ncy, shift, nbx, nby, dw, du);
+                word.resize(nb);
+                uni.resize(nb);
+                hipError_t e = hipGetLastError();
+                if (e == hipSuccess) e = hipMemcpy(word.data(), dw, nb * sizeof(uint64_t), hipMemcpyDeviceToHost);
+                if (e == hipSuccess) e = hipMemcpy(uni.data(), du, nb, hipMemcpyDeviceToHost);
+                (void)hipFree(dw);
+                (void)hipFree(du);
+                if (e != hipSuccess)
+                    return bail(fail(WGRT_ERR_HIP, std::string("coarse locator: ") + hipGetErrorString(e)));
+            }
+            CoarseHost ch;
+            coarse_table(word, uni, nbx, nby, shift, s->nfc, s->noc, ch);
+            std::vector<uint32_t> words(ch.bytes.size() / 4);
+            std::memcpy(words.data(), ch.bytes.data(), ch.bytes.size());
+            if ((st = upload(words, &s->d_coarse)) != WGRT_OK || (st = upload(ch.pal, &s->d_coarse_pal)) != WGRT_OK)
+                return bail(st);
+            s->coarse_shift = shift;
+            s->coarse_nbx = nbx;
+            s->coarse_nby = nby;
+            s->coarse_words = (int)words.size();
+            s->coarse_npal = ch.npal;
+            s->coarse_uniform = ch.uniform;
+        }
+    }
+    {
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         // resident workgroups of each instantiation (cell width x fused x single wavelength)
@@ -936,6 +1024,8 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_row_off);
     (void)hipFree(s->d_row_edges);
     (void)hipFree(s->d_bands);
+    (void)hipFree(s->d_coarse);
+    (void)hipFree(s->d_coarse_pal);
     for (auto &kv : s->scratch) {
         (void)hipFree(kv.second.ctr);
         (void)hipFree(kv.second.list);
@@ -960,6 +1050,11 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->n_polygons = s->npoly;
     info->device = s->device;
     info->jtile_bytes = (int64_t)s->jtile_d * 8;
+    info->coarse_shift = s->coarse_shift;
+    info->coarse_palette = s->coarse_npal;
+    info->coarse_blocks_x = s->coarse_nbx;
+    info->coarse_blocks_y = s->coarse_nby;
+    info->coarse_uniform = s->coarse_uniform;
     return WGRT_OK;
 }
 
@@ -1008,7 +1103,7 @@ wgrt_status ensure_scratch(wgrt_scene *ms, void *stream, int64_t n_rays, int num
         (void)hipFree(sc->part);
         sc->part = nullptr;
         sc->part_slots = 0;
-        hipError_t e = hipMalloc((void **)&sc->part, (size_t)slots * 4 * sizeof(unsigned long long));
+        hipError_t e = hipMalloc((void **)&sc->part, (size_t)slots * kPartWords * sizeof(unsigned long long));
         if (e != hipSuccess) return fail(WGRT_ERR_HIP, std::string("hipMalloc(launch scratch): ") + hipGetErrorString(e));
         sc->part_slots = slots;
     }
@@ -1082,7 +1177,11 @@ struct LaunchCfg {
     const int64_t *gid_blocks = nullptr;
     int64_t gid_block_rays = 0;
     const wgrt_debug_opts *dbg = nullptr;
+    double grid_k = 0.0;   // wgrt_launch_opts.grid_sqrt_k (0: kGridSqrtK; < 0: the resident grid)
 };
+
+// Single traces: ceil(kGridSqrtK * sqrt(work items)) workgroups (wgrt_launch_opts.grid_sqrt_k).
+constexpr double kGridSqrtK = 6.5;
 
 // One launch of the bounce kernel.  single: the single-wavelength kernel
 // process_rays_kernel_pro (GRTF:419-831) -- no lmd_num column, wavelength 0 of a
@@ -1172,6 +1271,11 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
     A.n_iter = 1;
+    A.coarse = s->d_coarse;
+    A.coarse_pal = s->d_coarse_pal;
+    A.coarse_shift = s->coarse_shift;
+    A.coarse_nx = s->coarse_nbx;
+    A.coarse_words = s->coarse_words;
     hipStream_t st = (hipStream_t)stream;
     if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
@@ -1186,18 +1290,16 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     // a workgroup's 4 waves need 4 work items to all have work (debug chunk_rays: smaller items)
     const int64_t item = (dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk;
     const int64_t useful = (n_rays + 4 * item - 1) / (4 * item);
-    if (c.workgroups <= 0 && !timeline && num_iter <= 1) {
+    if (c.workgroups <= 0 && !timeline && num_iter <= 1 && c.grid_k >= 0.0) {
         // a single trace ends with the drain of its longest ray chains, and chains run faster
         // on a less crowded chip, while the bulk before it wants every resident wave: the grid
         // that balances bulk throughput (work / W) against drain crowding (~ W) grows as
         // sqrt(work items).  K = 6.5 workgroups per sqrt(item), measured: C2
         // (1,936 items, 287 workgroups) -11 %, half and quarter C3 shards -8 / -12 %; C3 (946)
         // unchanged; C4 and larger keep the resident grid
-#ifndef WGRT_GRID_SQRT_K
-#define WGRT_GRID_SQRT_K 6.5
-#endif
+        const double K = c.grid_k > 0.0 ? c.grid_k : kGridSqrtK;
         const int64_t items = (n_rays + item - 1) / item;
-        const int64_t want = (int64_t)std::ceil(WGRT_GRID_SQRT_K * std::sqrt((double)items));
+        const int64_t want = std::max<int64_t>(1, (int64_t)std::ceil(K * std::sqrt((double)items)));
         if (grid > want) grid = want;
     }
     if (grid > useful) grid = useful;
@@ -1324,6 +1426,8 @@ wgrt_status wgrt_trace_opts(const wgrt_scene *s, const wgrt_rays *rays, int64_t 
     c.gid_blocks = opts->gid_blocks;
     c.gid_block_rays = opts->gid_block_rays;
     c.dbg = opts->debug;
+    c.grid_k = opts->grid_sqrt_k;
+    if (!(c.grid_k == c.grid_k)) return fail(WGRT_ERR_INVALID_ARGUMENT, "grid_sqrt_k is NaN");
     return trace_launch(s, rays, n_rays, gid_offset, rng_states, matrix_EB, stats, per_ray_bounces, stream, c);
 }
 
@@ -1437,6 +1541,44 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
     return WGRT_OK;
 }
 
+wgrt_status wgrt_debug_coarse_host(const wgrt_scene_desc *desc, double cell_mm, int coarse_shift, uint8_t *bytes_out,
+                                   int64_t bytes_cap, uint64_t *pal_out, int32_t *shift_out, int64_t *blocks_x,
+                                   int64_t *blocks_y, double *grid_out) {
+    if (!desc || !shift_out || !blocks_x || !blocks_y) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (!(cell_mm >= 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be >= 0");
+    SceneHost host;
+    try {
+        build_scene_host(*desc, cell_mm > 0.0 ? cell_mm : kDefaultCellMm, host, true, false);
+    } catch (const std::exception &e) {
+        return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
+    }
+    const LocatorHost &L = host.loc;
+    const int shift = coarse_shift_for(coarse_shift, L.ncx, L.ncy);
+    *shift_out = shift;
+    *blocks_x = *blocks_y = 0;
+    if (grid_out) {
+        grid_out[0] = L.x0;
+        grid_out[1] = L.y0;
+        grid_out[2] = L.h;
+        grid_out[3] = L.ncx;
+        grid_out[4] = L.ncy;
+    }
+    if (shift == 0) return WGRT_OK;
+    const int nbx = ((L.ncx - 1) >> shift) + 1, nby = ((L.ncy - 1) >> shift) + 1;
+    *blocks_x = nbx;
+    *blocks_y = nby;
+    if (!bytes_out && !pal_out) return WGRT_OK;
+    if (bytes_out && bytes_cap < (int64_t)nbx * nby) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes_cap too small");
+    std::vector<uint64_t> word;
+    std::vector<uint8_t> uni;
+    coarse_reduce_host(L.cells, L.ncx, L.ncy, shift, word, uni);
+    CoarseHost ch;
+    coarse_table(word, uni, nbx, nby, shift, (int)desc->n_fc_slices, (int)desc->n_oc_slices, ch);
+    if (bytes_out) std::memcpy(bytes_out, ch.bytes.data(), (size_t)nbx * nby);
+    if (pal_out) std::memcpy(pal_out, ch.pal.data(), 32 * sizeof(uint64_t));
+    return WGRT_OK;
+}
+
 wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int64_t bytes) {
     if (!s || !dst) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / dst");
     const size_t ncells = (size_t)s->loc_host.ncx * s->loc_host.ncy;
@@ -1446,9 +1588,12 @@ wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int
         case 0: src = s->d_cells, n = ncells * sizeof(uint64_t); break;
         case 1: src = s->d_tiles, n = (size_t)s->tiles * s->tile_d * sizeof(double); break;
         case 2: src = s->d_jtiles, n = (size_t)s->tiles * s->jtile_d * sizeof(double); break;
-        default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles");
+        case 3: src = s->d_coarse, n = (size_t)s->coarse_words * 4; break;
+        case 4: src = s->d_coarse_pal, n = s->d_coarse_pal ? 32 * sizeof(uint64_t) : 0; break;
+        default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles, 3 coarse table, 4 palette");
     }
     if (bytes != (int64_t)n) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes must be " + std::to_string(n));
+    if (n == 0) return WGRT_OK;
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return WGRT_OK;

@@ -51,15 +51,16 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
                     gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                     per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
                     workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1,
-                    gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None) -> None:
+                    gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None,
+                    grid_sqrt_k: float = 0.0) -> None:
     """Asynchronous launch on ``stream`` (default: torch's current stream).
 
     rays: dict of device float32 tensors keyed like the reference columns
     (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
     kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
     accepted too.  stats: optional int64[STATS_LEN] device tensor that is added to
-    (bounces, bad_rays, eyebox_hits, replayed, handoff_giveups; ``check_stats`` raises on a
-    hand-off give-up).  chunk_order: optional int32 device permutation of the 64-ray chunks
+    (bounces, bad_rays, eyebox_hits, replayed, handoff_giveups, interactions; ``check_stats`` raises
+    on a hand-off give-up).  chunk_order: optional int32 device permutation of the 64-ray chunks
     (``schedule_by_lifetime``); results do not depend on it.  num_iter: chained traces of every
     ray (the reference's ``num_iter`` loop of launches, MAIN:169-177) in one call -- results
     identical to ``num_iter`` calls; the Jones-vector variants run them in one persistent launch
@@ -67,13 +68,14 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
     several block ranges (int64 device tensor, first global id of each local block of
     ``gid_block_rays`` rays; ``gid_offset`` must then be 0).  debug: ``wgrt_debug_opts`` fields
     (cert_tol, cert_tol32, chunk_rays, timeline (uint64 device tensor), fail_after_trace,
-    handoff_wait_ticks) -- test / profiling hooks.
+    handoff_wait_ticks) -- test / profiling hooks.  grid_sqrt_k: the single-trace grid rule
+    (``wgrt_launch_opts.grid_sqrt_k``; 0 the default, < 0 the resident grid).
     """
     if scene.single_lambda:
         raise ValueError("trace_fullcolor needs a full-colour scene; use trace_single for a single-wavelength one")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
            workgroups, single=False, chunk_order=chunk_order, num_iter=num_iter, gid_blocks=gid_blocks,
-           gid_block_rays=gid_block_rays, debug=debug)
+           gid_block_rays=gid_block_rays, debug=debug, grid_sqrt_k=grid_sqrt_k)
 
 
 def new_stats(device) -> torch.Tensor:
@@ -103,7 +105,8 @@ def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: 
                  gid_offset: int = 0, n_rays: int | None = None, stats: torch.Tensor | None = None,
                  per_ray_bounces: torch.Tensor | None = None, stream=None, variant: int = VARIANT_AUTO,
                  workgroups: int = 0, chunk_order: torch.Tensor | None = None, num_iter: int = 1,
-                 gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None) -> None:
+                 gid_blocks: torch.Tensor | None = None, gid_block_rays: int = 0, debug: dict | None = None,
+                 grid_sqrt_k: float = 0.0) -> None:
     """One launch of the single-wavelength kernel (``process_rays_kernel_pro``, GRTF:419-831)
     through ``wgrt_trace_single_ex``: no ``lmd_num`` column (ignored if present),
     matrix_EB [NY, NX, 80, 120], branch guard ener * efficiency > 1e-15.  The scene must be
@@ -112,7 +115,7 @@ def trace_single(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_EB: 
         raise ValueError("trace_single needs a single-wavelength scene (Scene.from_geometry(..., wavelength=l))")
     _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
            workgroups, single=True, chunk_order=chunk_order, num_iter=num_iter, gid_blocks=gid_blocks,
-           gid_block_rays=gid_block_rays, debug=debug)
+           gid_block_rays=gid_block_rays, debug=debug, grid_sqrt_k=grid_sqrt_k)
 
 
 def _debug_opts(debug: dict | None):
@@ -135,7 +138,8 @@ def _debug_opts(debug: dict | None):
 
 
 def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ray_bounces, stream, variant,
-           workgroups, single, chunk_order=None, num_iter=1, gid_blocks=None, gid_block_rays=0, debug=None):
+           workgroups, single, chunk_order=None, num_iter=1, gid_blocks=None, gid_block_rays=0, debug=None,
+           grid_sqrt_k=0.0):
     device = torch.device("cuda", scene.device)
     x = rays["x"]
     N = x.numel() if n_rays is None else int(n_rays)
@@ -176,7 +180,7 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
                       n_chunks if chunk_order is not None else 0, int(num_iter),
                       ctypes.c_void_p(gid_blocks.data_ptr()) if gid_blocks is not None else None,
                       int(gid_block_rays) if gid_blocks is not None else 0,
-                      ctypes.pointer(dbg) if dbg is not None else None)
+                      ctypes.pointer(dbg) if dbg is not None else None, float(grid_sqrt_k))
     check(load().wgrt_trace_opts(
         scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
         ctypes.c_void_p(matrix_EB.data_ptr()),

@@ -13,9 +13,11 @@ Same flow as the reference script, on the MI355X kernel:
    at most ``FUSE_MAX_RAYS`` rays, else as separate launches (``fuse`` overrides), timed with HIP
    events (no JIT in the timed region, unlike the reference's wall clock);
 5. efficiencies ``A = sum(EB) / N / num_iter``, ``eff_c = 3 * sum(A[lambda])`` (MAIN:186-192)
-   and ``evaluation(EB / R / num_iter)`` (MAIN:197-198).
+   and ``evaluation(EB / R / num_iter)`` (MAIN:197-198);
+6. the "Eyebox Center View.png" export (MAIN:199-203): the evaluated image at the first eye row,
+   last eye column, as 8-bit RGB, rows flipped (``eyebox_center_view``, written without OpenCV).
 
-Plots and the PNG export (MAIN:199-237) are visual-only and not reproduced.
+The matplotlib plots (MAIN:213-237) are visual-only and not reproduced.
 Multi-GPU: run under ``torch.distributed.run``; each rank traces an interleaved set of FoV x
 wavelength blocks and the eyebox slabs are gathered to rank 0 (``distributed.py``).
 """
@@ -39,7 +41,10 @@ FUSE_MAX_RAYS = 4_000_000
 def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000, num_iter: int = 4,
         lambdas=(0, 1, 2), lut_dir: str | None = None, lut_seed: int = 0, lut_profile: str = "default",
         point_seed: int | None = None, evaluate: bool = True, verbose: bool = True, variant: int = 0,
-        fuse: bool | None = None) -> dict:
+        fuse: bool | None = None, points: np.ndarray | None = None, png: str | None = None) -> dict:
+    """The reference script's job on this engine; returns its printed quantities and arrays.
+    ``points``: the R/2 in-coupler origins to use (default: sampled, GRTF:12-23, seeded by
+    ``point_seed``); ``png``: where to write the "Eyebox Center View" image (needs ``evaluate``)."""
     import torch
     import torch.distributed as dist
 
@@ -66,7 +71,9 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
     scene = Scene.from_geometry(geom, luts, device=dev.index, lut_f32_angles=f32_angles)
     R = int(num_rays_per_FoV)
     rng_pts = np.random.default_rng(point_seed) if point_seed is not None else None
-    points = generate_points_in_polygon(geom.IC, R // 2, rng=rng_pts)
+    if points is None:
+        points = generate_points_in_polygon(geom.IC, R // 2, rng=rng_pts)
+    points = np.ascontiguousarray(points, dtype=np.float64)
     if world > 1:  # every rank must use the same origins
         t = torch.from_numpy(np.ascontiguousarray(points)).to(dev)
         dist.broadcast(t, src=0)
@@ -121,11 +128,60 @@ def run(num_FOV_x: int = 100, num_FOV_y: int = 75, num_rays_per_FoV: int = 5000,
         from .AR_system_evaluation_functions import evaluation
         delta_e, U_fov, U_EB, output_image = evaluation(matrix_EB / R / num_iter)
         out.update(delta_e=float(delta_e), U_fov=float(U_fov), U_EB=float(U_EB), output_image=output_image)
+        out["center_view"] = eyebox_center_view(output_image)
+        if png:
+            write_png(png, out["center_view"])
+            say(f"Wrote {png}")
         say(f"Color dispersion      : {delta_e:8.2f}")
         say(f"FoV uniformity        : {U_fov * 100:8.2f} %")
         say(f"Eyebox uniformity     : {U_EB * 100:8.2f} %")
     scene.close()
     return out
+
+
+def eyebox_center_view(output_image: np.ndarray) -> np.ndarray:
+    """The image MAIN:199-203 exports: ``output_image[:, :, :, 0, n_epx - 1]`` (first eye row, last eye
+    column) as uint8 (``* 255`` then truncation), rows flipped -- uint8 RGB [n_FOVy, n_FOVx, 3].  (The
+    reference converts it to BGR for cv2.imwrite, which stores the RGB image in the PNG.)"""
+    n_epx = output_image.shape[4]
+    return np.ascontiguousarray(np.flipud((output_image[:, :, :, 0, n_epx - 1] * 255).astype(np.uint8)))
+
+
+def write_png(path: str, rgb: np.ndarray) -> None:
+    """8-bit RGB PNG (filter 0 on every row, zlib), without OpenCV / PIL."""
+    import struct
+    import zlib
+    a = np.ascontiguousarray(rgb, dtype=np.uint8)
+    if a.ndim != 3 or a.shape[2] != 3:
+        raise ValueError("expected an [H, W, 3] uint8 image")
+    h, w = a.shape[:2]
+
+    def chunk(tag, data):
+        return struct.pack(">I", len(data)) + tag + data + struct.pack(">I", zlib.crc32(tag + data) & 0xFFFFFFFF)
+    raw = b"".join(b"\x00" + a[r].tobytes() for r in range(h))
+    with open(path, "wb") as f:
+        f.write(b"\x89PNG\r\n\x1a\n" + chunk(b"IHDR", struct.pack(">IIBBBBB", w, h, 8, 2, 0, 0, 0)) +
+                chunk(b"IDAT", zlib.compress(raw, 9)) + chunk(b"IEND", b""))
+
+
+def read_png(path: str) -> np.ndarray:
+    """Decoder of write_png's files (8-bit RGB, filter 0), for the tests."""
+    import struct
+    import zlib
+    data = open(path, "rb").read()
+    assert data[:8] == b"\x89PNG\r\n\x1a\n"
+    pos, idat, w, h = 8, b"", 0, 0
+    while pos < len(data):
+        n, tag = struct.unpack(">I4s", data[pos:pos + 8])
+        body = data[pos + 8:pos + 8 + n]
+        if tag == b"IHDR":
+            w, h = struct.unpack(">II", body[:8])
+        elif tag == b"IDAT":
+            idat += body
+        pos += 12 + n
+    raw = np.frombuffer(zlib.decompress(idat), np.uint8).reshape(h, 1 + 3 * w)
+    assert (raw[:, 0] == 0).all()
+    return raw[:, 1:].reshape(h, w, 3).copy()
 
 
 def main(argv=None):
@@ -143,6 +199,8 @@ def main(argv=None):
                     help="num_iter chained traces as one fused launch (auto: when a GPU traces <= 4M rays)")
     ap.add_argument("--no-fuse", action="store_true", help="same as --fuse no")
     ap.add_argument("--json", default=None, help="write scalar results here")
+    ap.add_argument("--png", default="Eyebox Center View.png",
+                    help="the eyebox-center image (MAIN:199-203); empty string: do not write it")
     a = ap.parse_args(argv)
     import torch
     import torch.distributed as dist
@@ -152,7 +210,8 @@ def main(argv=None):
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     res = run(a.num_fov_x, a.num_fov_y, a.rays_per_fov, a.num_iter, lut_dir=a.lut_dir, lut_seed=a.lut_seed,
               lut_profile=a.lut_profile, point_seed=a.point_seed, evaluate=not a.no_eval,
-              fuse=False if a.no_fuse else {"auto": None, "yes": True, "no": False}[a.fuse])
+              fuse=False if a.no_fuse else {"auto": None, "yes": True, "no": False}[a.fuse],
+              png=a.png or None)
     if a.json and (not dist.is_initialized() or dist.get_rank() == 0):
         keep = {k: v for k, v in res.items() if isinstance(v, (int, float, dict, str))}
         with open(a.json, "w") as f:

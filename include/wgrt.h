@@ -36,7 +36,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 4
+#define WGRT_ABI_VERSION 5
 
 typedef enum {
     WGRT_OK = 0,
@@ -100,6 +100,10 @@ typedef struct {
                                   wgrt_launch_opts.num_iter.  Never in a correct
                                   run: a nonzero count means the eyebox grid and the RNG states of
                                   this call are wrong, and the Python layer raises on it.           */
+    uint64_t interactions;     /* ABI 5.  Monte-Carlo interactions of the bounce loop (the iterations of
+                                  GRTF:905 that draw: coupler hits in R0..R5).  The other bounces are the
+                                  in-coupling events (one per traced ray, GRTF:860-904) and the iterations
+                                  without a draw: miss hops, R3 -> R4 switches, terminations.          */
 } wgrt_trace_stats;
 
 typedef struct {
@@ -111,6 +115,11 @@ typedef struct {
     int32_t n_polygons;
     int32_t device;
     int64_t jtile_bytes;       /* Jones-vector tile per (lambda, FoV) (variants 7 / 9)  */
+    /* ABI 5: the coarse locator of the hop runs (wgrt_scene_opts.coarse_shift) */
+    int32_t coarse_shift;      /* blocks of 2^coarse_shift x 2^coarse_shift locator cells; 0 = off */
+    int32_t coarse_palette;    /* distinct cell words the uniform blocks hold (<= 31)              */
+    int64_t coarse_blocks_x, coarse_blocks_y;
+    int64_t coarse_uniform;    /* blocks answered on chip (one EDGE-free cell word in every cell)  */
 } wgrt_scene_info;
 
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon
@@ -129,6 +138,12 @@ typedef struct {
                              scene's cosines of that table's angles are cosf of the float32 angle,
                              widened.  The coefficients themselves enter E_field_cal widened exactly, as
                              numba promotes complex64 x complex128.  0: double-precision cos (complex128). */
+    int coarse_shift;     /* ABI 5.  Hop runs of the Jones-vector variants: a block of
+                             2^coarse_shift x 2^coarse_shift locator cells whose cells all hold one cell word
+                             without an EDGE class is answered from a byte table in LDS, and a ray's miss hops
+                             (GRTF:1049-1052, 1105-1108, 1175-1178) that land in such blocks run inside one
+                             pass of the wave loop.  0 = default (5: 1/4-mm blocks at the default cell), made
+                             coarser until the table fits the LDS budget; -1 = off.  Results are identical. */
 } wgrt_scene_opts;
 wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const wgrt_scene_opts *opts,
                                  wgrt_scene **out);
@@ -211,6 +226,11 @@ typedef struct {
     const int64_t *gid_blocks;
     int64_t gid_block_rays;
     const wgrt_debug_opts *debug;   /* NULL in production (include/wgrt_debug.h) */
+    /* ABI 5.  Single traces (num_iter <= 1) with workgroups == 0: the persistent grid is
+     * ceil(grid_sqrt_k * sqrt(work items)) workgroups, at most the resident grid (a single trace
+     * ends with the drain of its longest ray chains, which run faster on a less crowded chip;
+     * DESIGN.md §5.4).  0 = the default 6.5; a negative value = the resident grid. */
+    double grid_sqrt_k;
 } wgrt_launch_opts;
 
 /* One launch of either bounce kernel with launch options (everything else as

@@ -34,6 +34,14 @@
 #include "wgrt_oracle.h"
 
 #define PI_D 3.141592653589793
+
+/* Analysis hook (tools/hop_runs.c includes this file with its own definition): one call per
+ * bounce event -- ev 0 interaction at (x, y) before the branch moves the ray, 1 miss hop from (x, y)
+ * by (gx, gy), 2 the R3 -> R4 switch, 3 termination by the loop-top eff_reg1 test or an R5 miss.
+ * A no-op in the oracle library. */
+#ifndef ORACLE_EV
+#define ORACLE_EV(ev, region, x, y, gx, gy) ((void)0)
+#endif
 #define EB_NY 80
 #define EB_NX 120
 
@@ -224,6 +232,7 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
         double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_IC2, th_ic2) / lcos(sc, T_IC1, th_ic1) * n_g;
         double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_IC3, th_ic3) / lcos(sc, T_IC1, th_ic1) * n_g;
         double u = rng_draw(&s, gid);
+        ORACLE_EV(0, 9, st.x, st.y, 0.0, 0.0);
         if (u <= e1) {
             take(&st, &E1, lcos(sc, T_IC2, th_ic2), tir[0], gap + 0);
             st.ener *= e1;
@@ -241,7 +250,11 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
 
     for (int64_t it = 0; it < 100000; ++it) {
         ++bounces;
-        if (!inside_or_on_edge(st.x, st.y, sc->eff1, sc->n_eff1)) { why = (uint8_t)(10 * region + 1); goto done; }
+        if (!inside_or_on_edge(st.x, st.y, sc->eff1, sc->n_eff1)) {
+            ORACLE_EV(3, region, st.x, st.y, 0.0, 0.0);
+            why = (uint8_t)(10 * region + 1);
+            goto done;
+        }
         double cd = cos(st.dph), sd = sin(st.dph);
         if (region == 0 || region == 1) {
             /* GRTF:908-999 */
@@ -260,6 +273,7 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
             double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_IC2, th_ic2) / st.cos_th;
             double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_IC3, th_ic3) / st.cos_th;
             double u = rng_draw(&s, gid);
+            ORACLE_EV(0, region, st.x, st.y, 0.0, 0.0);
             if (u <= e1) {
                 take(&st, &E1, lcos(sc, T_IC2, th_ic2), tir[0], gap + 0);
                 st.ener *= e1;
@@ -299,6 +313,7 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_FC2, th2) / st.cos_th;
                 double en1 = st.ener * e1, en2 = st.ener * e2;
                 double u = rng_draw(&s, gid);
+                ORACLE_EV(0, region, st.x, st.y, 0.0, 0.0);
                 if (u <= e1 && en1 > sc->threshold) {
                     take(&st, &E1, lcos(sc, T_FC1, th1), tir[0], gap + 0);
                     st.ener = en1 * 1.0;
@@ -315,12 +330,15 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
             }
             if (!hit) {
                 if (region == 2) {
+                    ORACLE_EV(1, region, st.x, st.y, st.gx, st.gy);
                     st.x += st.gx;
                     st.y += st.gy;
                     st.dph += 2 * tir[0];
                 } else if (!inside_or_on_edge(st.x, st.y, sc->eff2, sc->n_eff2)) {
+                    ORACLE_EV(2, region, st.x, st.y, 0.0, 0.0);
                     region = 4;
                 } else {
+                    ORACLE_EV(1, region, st.x, st.y, st.gx, st.gy);
                     st.x += st.gx;
                     st.y += st.gy;
                     st.dph += 2 * tir[1];
@@ -357,6 +375,7 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e3 = (E3.te * E3.te + E3.tm * E3.tm) * lcos(sc, T_IC1, th_ic1) / st.cos_th / n_g;
                 double en1 = st.ener * e1, en2 = st.ener * e2, en3 = st.ener * e3;
                 double u = rng_draw(&s, gid);
+                ORACLE_EV(0, region, st.x, st.y, 0.0, 0.0);
                 if (u <= e1 && en1 > sc->threshold) {
                     take(&st, &E1, lcos(sc, T_OC1, th1), tir[1], gap + 2);
                     st.ener = en1 * 1.0;
@@ -377,7 +396,12 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 break;
             }
             if (!hit) {
-                if (region == 5) { why = 55; goto done; }
+                if (region == 5) {
+                    ORACLE_EV(3, region, st.x, st.y, 0.0, 0.0);
+                    why = 55;
+                    goto done;
+                }
+                ORACLE_EV(1, region, st.x, st.y, st.gx, st.gy);
                 st.x += st.gx;
                 st.y += st.gy;
                 st.dph += 2 * tir[1];

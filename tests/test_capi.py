@@ -3,6 +3,7 @@ symbol include/wgrt.h declares, and rejects malformed scenes before touching the
 import ctypes
 import os
 import re
+import subprocess
 
 import numpy as np
 import pytest
@@ -43,12 +44,28 @@ def test_no_process_wide_debug_setters(lib):
         assert not hasattr(lib, name), name
 
 
-def test_struct_layouts_match_header():
-    """ctypes mirrors of the option / stats structs have the C sizes (x86-64 / gfx950 host ABI)."""
-    assert ctypes.sizeof(_lib.TraceStats) == 5 * 8
-    assert ctypes.sizeof(_lib.LaunchOpts) == 4 * 3 + 4 + 8 + 8 + 4 + 4 + 8 + 8 + 8
-    assert ctypes.sizeof(_lib.DebugOpts) == 8 + 8 + 4 + 4 + 8 + 8 + 4 + 4 + 8
-    assert ctypes.sizeof(_lib.SceneOpts) == 16
+def test_struct_layouts_match_header(tmp_path):
+    """ctypes mirrors of the ABI structs have the C compiler's sizes and field offsets (gcc on the
+    headers themselves, x86-64 host ABI)."""
+    structs = {"wgrt_trace_stats": _lib.TraceStats, "wgrt_launch_opts": _lib.LaunchOpts,
+               "wgrt_debug_opts": _lib.DebugOpts, "wgrt_scene_opts": _lib.SceneOpts,
+               "wgrt_scene_info": _lib.SceneInfo, "wgrt_scene_desc": _lib.SceneDesc, "wgrt_rays": _lib.Rays,
+               "wgrt_shadow_stats": _lib.ShadowStats}
+    lines = ['#include <stdio.h>', '#include <stddef.h>', '#include "wgrt_debug.h"', "int main(void) {"]
+    for c, py in structs.items():
+        lines.append(f'printf("{c} %zu\\n", sizeof({c}));')
+        for f, _ in py._fields_:
+            lines.append(f'printf("{c}.{f} %zu\\n", offsetof({c}, {f}));')
+    lines.append("return 0; }")
+    src = tmp_path / "layout.c"
+    src.write_text("\n".join(lines))
+    exe = tmp_path / "layout"
+    subprocess.run(["gcc", "-std=c99", "-I", os.path.join(REPO, "include"), str(src), "-o", str(exe)], check=True)
+    got = dict(l.split() for l in subprocess.run([str(exe)], capture_output=True, text=True, check=True).stdout.split("\n") if l)
+    for c, py in structs.items():
+        assert int(got[c]) == ctypes.sizeof(py), c
+        for f, _ in py._fields_:
+            assert int(got[f"{c}.{f}"]) == getattr(py, f).offset, f"{c}.{f}"
 
 
 def test_abi_version_and_status_strings(lib):

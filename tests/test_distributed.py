@@ -97,7 +97,7 @@ def _bench_worker(rank, world, port, outdir, assign, collect):
     shard = make_shard(NX, NY, len(LAMBDAS), R, world, rank, assign)
     rays, rng_t = _host_builder(pts)(shard)
     eb = torch.zeros((3, NY, NX, 80, 120), dtype=torch.float32)
-    stats = torch.zeros(5, dtype=torch.int64)
+    stats = torch.zeros(6, dtype=torch.int64)
     calls = []
     hook = lambda j, what: calls.append((j, what))
     el, tot, loc = timed_run(_oracle_tracer(geom, luts, stats), rays, rng_t, eb, shard.gid, NUM_ITER, 1, stats,
@@ -111,7 +111,7 @@ def _bench_worker(rank, world, port, outdir, assign, collect):
 
 
 def _replica_worker(rank, world, port, outdir):
-    """bench.py --gpus N's default (weak scaling): rank r traces the whole batch as replica r
+    """bench.py --gpus N's ``weak`` record (and --scaling weak): rank r traces the whole batch as replica r
     (global ids r * N + i) through timed_run, and the eyebox grids are sum-reduced to rank 0."""
     os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
     dist.init_process_group("gloo", rank=rank, world_size=world)
@@ -120,7 +120,7 @@ def _replica_worker(rank, world, port, outdir):
     rays, rng = shard_rays_host(pts, NX, NY, LAMBDAS, R, shard.blocks, gid_base=shard.gid_base)
     rng_t = torch.from_numpy(rng.view(np.int32))
     eb = torch.zeros((3, NY, NX, 80, 120), dtype=torch.float32)
-    stats = torch.zeros(5, dtype=torch.int64)
+    stats = torch.zeros(6, dtype=torch.int64)
     el, tot, loc = timed_run(_oracle_tracer(geom, luts, stats), rays, rng_t, eb, shard.gid, NUM_ITER, 1, stats)
     np.save(os.path.join(outdir, f"rng{rank}.npy"), rng_t.numpy())
     np.save(os.path.join(outdir, f"res{rank}.npy"), np.array([el, tot, loc], dtype=np.float64))
@@ -147,19 +147,20 @@ def _check_rng(tmp_path, world, rng):
         np.testing.assert_array_equal(got, want, err_msg=f"rank {r}")
 
 
-@pytest.mark.parametrize("assign,collect", [("interleaved", "gather"), ("contiguous", "reduce")])
-def test_bench_timed_region_sharded(tmp_path, assign, collect):
-    """bench.py --gpus 2's code path (shard, chained calls bracketed by the event hook, eyebox
-    collective, MAX time / SUM bounces all-reduces) gives the single-process job's bounces, grid and
-    RNG states."""
-    world = 2
+@pytest.mark.parametrize("world,assign,collect", [(2, "interleaved", "gather"), (3, "interleaved", "gather"),
+                                                  (2, "contiguous", "reduce")])
+def test_bench_timed_region_sharded(tmp_path, world, assign, collect):
+    """bench.py --gpus N's default (--scaling strong: the metric's one batch split over the ranks as
+    interleaved FoV x wavelength blocks, eyebox slabs gathered to rank 0): shard, chained calls
+    bracketed by the event hook, eyebox collective, MAX time / SUM bounces all-reduces -- gives the
+    single-process job's bounces, grid and RNG states."""
     mp.start_processes(_bench_worker, args=(world, _free_port(), str(tmp_path), assign, collect), nprocs=world,
                        join=True, start_method="spawn")
     rng, eb, tot = _single_process()
     res = [np.load(tmp_path / f"res{r}.npy") for r in range(world)]
     assert all(int(r[1]) == tot for r in res)                 # SUM over ranks, on every rank
     assert sum(int(r[2]) for r in res) == tot and all(r[2] > 0 for r in res)
-    assert res[0][0] == res[1][0] > 0                         # MAX over ranks
+    assert all(r[0] == res[0][0] for r in res) and res[0][0] > 0   # MAX over ranks
     assert all(int(r[3]) == 2 * NUM_ITER for r in res)        # start + end hook per call
     np.testing.assert_array_equal(np.load(tmp_path / "eb.npy"), eb)
     _check_rng(tmp_path, world, rng)
@@ -177,7 +178,7 @@ def test_sharded_job_equals_single_process(tmp_path, world, assign, collect):
 
 
 def test_replicas_equal_tiled_single_process(tmp_path):
-    """Weak scaling (bench.py's default at N > 1): N replicas of the batch with global ids offset
+    """Weak scaling (bench.py's ``weak`` record at N > 1): N replicas of the batch with global ids offset
     per rank give exactly the single-process trace of the batch's columns tiled N times (RNG seeded
     by global index, MAIN:158): every rank's RNG states, the SUM of bounces and the reduced grid."""
     world = 2

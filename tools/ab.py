@@ -25,7 +25,8 @@ w = CONFIGS[os.environ["AB_CONFIG"]]
 nx, ny, lam, R = w.nx, w.ny, list(w.lambdas), w.R
 dev = torch.device("cuda", 0)
 g, L, pts = build_inputs(w)
-sc = Scene.from_geometry(g, L)
+sc = Scene.from_geometry(g, L, **json.loads(os.environ.get("AB_SCENE") or "{}"))
+lk = json.loads(os.environ.get("AB_LAUNCH") or "{}")
 rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(make_shard(nx, ny, len(lam), R, 1, 0))
 eb = torch.zeros(sc.eb_shape(), dtype=torch.float32, device=dev)
 st = new_stats(dev)
@@ -44,13 +45,13 @@ if os.environ.get("AB_ORDER"):   # lifetime-ordered chunk issue from one earlier
         cnt = torch.zeros(nx * ny * 3, device=dev).index_add_(0, key, torch.ones_like(pb, dtype=torch.float32))
         ck = (tot / cnt.clamp_min(1))[key[::CHUNK]]
         order = torch.argsort(-ck, stable=True).to(torch.int32)
-for _ in range(3): trace_fullcolor(sc, rays, rng, eb, chunk_order=order)
+for _ in range(3): trace_fullcolor(sc, rays, rng, eb, chunk_order=order, **lk)
 trace_fullcolor(sc, rays, rng, eb, num_iter=2)
 torch.cuda.synchronize()
 ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(nl + 1)]
 st.zero_()
 for k in range(nl):
-    ev[k][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st, chunk_order=order); ev[k][1].record()
+    ev[k][0].record(); trace_fullcolor(sc, rays, rng, eb, stats=st, chunk_order=order, **lk); ev[k][1].record()
 torch.cuda.synchronize()
 b1 = int(st[0]) / nl
 st.zero_()
@@ -73,11 +74,19 @@ def main():
     res = {n: [] for n in a.names}
     for r in range(a.rounds):
         for n in a.names:
-            # NAME[:seg|:glob]: the build, optionally with lifetime-ordered chunk issue
-            build, _, order = n.partition(":")
+            # NAME[:seg|:glob][@scene_opt=v,...][+launch_opt=v,...]: the build ("tree" = the in-tree
+            # library), optionally with lifetime-ordered chunk issue, scene options (e.g. coarse_shift=-1)
+            # and launch options (e.g. grid_sqrt_k=4.5)
+            n0, _, lopts = n.partition("+")
+            n0, _, sopts = n0.partition("@")
+            build, _, order = n0.partition(":")
+            num = lambda v: float(v) if "." in v else int(v)
+            scene_kw = {k: num(v) for k, v in (kv.split("=") for kv in sopts.split(",") if kv)}
+            launch_kw = {k: num(v) for k, v in (kv.split("=") for kv in lopts.split(",") if kv)}
             lib = os.path.join(REPO, "exp_libs", build, "libwgrt.so") if build != "tree" else ""
             env = dict(os.environ, REPO=REPO, AB_CONFIG=a.config, AB_LAUNCHES=str(a.launches),
-                       AB_FUSED=str(a.fused), WGRT_LIB=lib, AB_ORDER=order)
+                       AB_FUSED=str(a.fused), WGRT_LIB=lib, AB_ORDER=order, AB_SCENE=json.dumps(scene_kw),
+                       AB_LAUNCH=json.dumps(launch_kw))
             p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(p.stderr[-3000:])
