@@ -19,7 +19,8 @@ Workloads (``--config``, BASELINE.json configs, configs.py):
     C2  single-lambda 532 nm, 11x11 FoV, num_rays_per_FoV = 1024
     C3  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 1024 (the metric's workload)
     C4  full-colour 21x21 FoV x 3 lambda, num_rays_per_FoV = 4096
-    C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce stress
+    C5  full-colour 41x41 FoV x 3 lambda, num_rays_per_FoV = 16384, deep-bounce stress (hops x 0.05)
+    C5d the C5 batch on the design geometry (unscaled hops)
     auto (default) = C3: the metric's workload.
 Multi-GPU: one process per GPU through distributed.py.
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
@@ -60,7 +61,7 @@ def parse(argv=None):
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=LONG_STEPS)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--config", default="auto", choices=["auto", "C2", "C3", "C4", "C5"])
+    ap.add_argument("--config", default="auto", choices=["auto", "C2", "C3", "C4", "C5", "C5d"])
     ap.add_argument("--lut-seed", type=int, default=0)
     ap.add_argument("--variant", type=int, default=0, help="kernel variant (include/wgrt.h); 0 auto")
     ap.add_argument("--scaling", default="strong", choices=["weak", "strong"],

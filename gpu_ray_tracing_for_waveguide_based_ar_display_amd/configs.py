@@ -9,7 +9,9 @@ C5, "deep-bounce stress", uses the ``stress`` LUT profile (higher 0th-order refl
 out-coupling, a better in-coupler) on a waveguide 20x thinner than the design's (every hop of
 ``lut_gap`` = 2 t tan(theta), CC:656-687, scaled by 0.05): rays live 50 bounces on average
 instead of C3's 6.4, and the batch's tail reaches past 1,000 bounces, so the certification's
-depth term is exercised where it grows.
+depth term is exercised where it grows.  The short hops also make consecutive
+locator lookups of a ray hit nearby cells, so C5's rate is not comparable with C3 / C4's; C5d is
+the same stress batch on the design geometry (CC:140, t = 0.7 mm, hops unscaled).
 """
 from __future__ import annotations
 
@@ -59,6 +61,9 @@ CONFIGS = {
     "C5": Workload("C5", "BASELINE config 5: full-colour 41x41 FoV x 3 λ, num_rays_per_FoV=16384, deep-bounce stress "
                          "(stress LUT, hops x0.05), FoV x λ sharded", 41, 41, (0, 1, 2), 16384, profile="stress",
                    gap_scale=0.05),
+    "C5d": Workload("C5d", "BASELINE config 5 on the design geometry: full-colour 41x41 FoV x 3 λ, "
+                           "num_rays_per_FoV=16384, stress LUT, unscaled hops (t = 0.7 mm, CC:140)", 41, 41, (0, 1, 2),
+                    16384, profile="stress"),
 }
 
 

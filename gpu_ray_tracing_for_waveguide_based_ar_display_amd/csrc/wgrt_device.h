@@ -73,7 +73,8 @@ struct TraceArgs {
     int n_iter;
     uint64_t *rng64;
     uint32_t iter_epoch;
-    unsigned long long handoff_wait_ticks;   // fused: s_memrealtime ticks a lane may wait for a hand-off
+    unsigned long long handoff_wait_ticks;   // fused: s_memrealtime ticks a lane may wait for a hand-off ...
+    uint32_t handoff_min_passes;             // ... once its wave has also run this many passes waiting
     // global ray ids of an interleaved shard (wgrt_launch_opts.gid_blocks): NULL = gid_offset + i
     const int64_t *gid_blocks;
     int64_t gid_block_rays;

@@ -187,6 +187,10 @@ constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queu
 // (epoch / tag) into a visible count within seconds instead of a hung GPU; it cannot be ms
 // without failing legitimate 1e5-bounce rays.
 constexpr unsigned long long kHandoffTicksPerIter = 100000000ull;   // s_memrealtime: 100 MHz
+// ... and the waiting lane's own wave must also have run this many passes since the wait began: the
+// clock runs while a wave is preempted or time-sliced (another queue, CWSR, profiler replay), its
+// passes do not, so a waiter that was merely descheduled does not give a correct hand-off up
+constexpr uint32_t kHandoffMinPasses = 4096;
 
 // A wave-uniform copy of v (lane 0's value, in SGPRs): the wave loop's queue state is uniform,
 // and keeping it scalar lets its branches be scalar branches instead of exec-mask juggling.
@@ -255,6 +259,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     // could overflow (2^31 bounces on one lane: never in practice)
     uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0, tot_int = 0;
     unsigned long long wait_t0 = 0;    // fused: when this lane started waiting for its ray (s_memrealtime)
+    uint32_t wait_passes = 0;          // ... and the wave's passes since then
     unsigned long long qbase = 0;      // this wave's block of out-coupling slots ...
     int qfill = kQBlock;               // ... and how many of them are used (none reserved yet)
     bool qblk = false;                 // a block has been reserved
@@ -316,6 +321,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             } else {
                 waiting = true;
                 wait_t0 = __builtin_amdgcn_s_memrealtime();
+                wait_passes = 0;
                 return;
             }
         }
@@ -425,9 +431,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 entry = true;
             } else if ((tag >> 8) == ((A.iter_epoch << 1) | 1u)) {
                 waiting = false;   // abandoned in an earlier iteration: the replay kernel finishes it
-            } else if (__builtin_amdgcn_s_memrealtime() - wait_t0 > A.handoff_wait_ticks) {
+            } else if ((++wait_passes > A.handoff_min_passes) &
+                       (__builtin_amdgcn_s_memrealtime() - wait_t0 > A.handoff_wait_ticks)) {
                 waiting = false;   // hand-off never arrived: give the trace up, visibly
                 ++tot_giveup;
+                // and mark the ray abandoned from this trace on, so that its later traces skip it instead of
+                // each waiting out the bound again (the call's results are invalid; the Python layer raises)
+                __hip_atomic_store(KA(rng64) + L.i, (uint64_t)iter_tag(A.iter_epoch, L.k, true), __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_AGENT);
             }
         }
         uint64_t need = __ballot(!active && !waiting);
@@ -821,6 +832,13 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
     const bool host_build = opts && opts->host_build != 0;
     const int f32_angles = opts ? opts->lut_f32_angles : 0;
     if (f32_angles & ~0x7f) return fail(WGRT_ERR_INVALID_ARGUMENT, "lut_f32_angles has bits beyond the 7 LUTs");
+    // A mixed set: compiled numba unifies the ray's theta (assigned from every table, GRTF:850, 872, 1021,
+    // ...) to complex128 as soon as one table is complex128, so the carried cos(theta.real) would be a
+    // double cosine of a single-precision table's angle while that table's numerator stays cosf --
+    // two cosines per branch the scene does not hold.  Only uniform sets are supported.
+    if (f32_angles != 0 && f32_angles != 0x7f)
+        return fail(WGRT_ERR_UNSUPPORTED, "lut_f32_angles must be 0 (complex128 LUTs) or 0x7f (all seven complex64): "
+                                          "a mixed-precision LUT set is not supported");
     // host: validation, the locator's geometry (extent, vertices, row bands) and the trig table
     // (every cos / sin on the host libm); the cell words and the tiles are built on the device
     // (host_build: both on the host, the reference build the device one is checked against)
@@ -1318,6 +1336,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         A.iter_epoch = epoch;
         A.handoff_wait_ticks = (dbg && dbg->handoff_wait_ticks) ? dbg->handoff_wait_ticks
                                                                 : kHandoffTicksPerIter * (unsigned long long)(num_iter + 1);
+        // a debug bound (fault-injection tests) gives up on the clock alone
+        A.handoff_min_passes = (dbg && dbg->handoff_wait_ticks) ? 0u : kHandoffMinPasses;
     }
     A.replay_count = ctr + kHeads * kHeadStride;
     A.replay_list = sc->list;

@@ -79,6 +79,16 @@ class GidMap:
             return 0
         return int(b[0]) if np.array_equal(b, b[0] + R * np.arange(len(b))) else None
 
+    def device_blocks(self, device):
+        """``block_gid`` as an int64 tensor on ``device`` (wgrt_launch_opts.gid_blocks), uploaded on first
+        use and cached on this map."""
+        import torch
+        cache = self.__dict__.setdefault("_dev", {})
+        key = str(device)
+        if key not in cache:
+            cache[key] = torch.as_tensor(self.block_gid, dtype=torch.int64, device=device)
+        return cache[key]
+
     def runs(self):
         """Consecutive stretches: ``(local_ray_lo, local_ray_hi, global_gid_lo)``."""
         b, R = self.block_gid, self.rays_per_block
@@ -327,22 +337,17 @@ def timed_run(trace_fn, rays, rng, eb, gid: GidMap, steps: int, per_call: int, s
 def hip_tracer(scene, variant: int = 0, stats=None):
     """trace_fn for ``run_steps`` / ``trace_job`` using the HIP kernel (torch device tensors);
     ``stats`` (int64[STATS_LEN] device tensor) is added to by every call.  A shard of several
-    block ranges passes its global ids as ``gid_blocks`` (uploaded once per map)."""
-    import torch
-
+    block ranges passes its global ids as ``gid_blocks``, uploaded once per map and device and kept
+    on the GidMap itself (``GidMap.device_blocks``: released with the map, no tracer-side cache)."""
     from .engine import trace_fullcolor
-    cache = {}
 
     def fn(rays, rng, eb, gid: GidMap, num_iter=1):
         off = gid.offset
         if off is not None:
             trace_fullcolor(scene, rays, rng, eb, gid_offset=off, stats=stats, variant=variant, num_iter=num_iter)
             return
-        key = id(gid)
-        if key not in cache:
-            cache[key] = (gid, torch.as_tensor(gid.block_gid, dtype=torch.int64, device=rng.device))
         trace_fullcolor(scene, rays, rng, eb, stats=stats, variant=variant, num_iter=num_iter,
-                        gid_blocks=cache[key][1], gid_block_rays=gid.rays_per_block)
+                        gid_blocks=gid.device_blocks(rng.device), gid_block_rays=gid.rays_per_block)
     return fn
 
 

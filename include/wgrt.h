@@ -137,7 +137,10 @@ typedef struct {
                              in single precision (GRTF:866-869 and every cos ratio after it), so the
                              scene's cosines of that table's angles are cosf of the float32 angle,
                              widened.  The coefficients themselves enter E_field_cal widened exactly, as
-                             numba promotes complex64 x complex128.  0: double-precision cos (complex128). */
+                             numba promotes complex64 x complex128.  0: double-precision cos (complex128).
+                             ABI 5: only 0 and 0x7f (all seven tables complex64) are accepted; a mixed set
+                             is WGRT_ERR_UNSUPPORTED (numba would carry the ray's angle as complex128 while a
+                             complex64 table's own cosine stays float32: see wgrt_scene_create_ex). */
     int coarse_shift;     /* ABI 5.  Hop runs of the Jones-vector variants: a block of
                              2^coarse_shift x 2^coarse_shift locator cells whose cells all hold one cell word
                              without an EDGE class is answered from a byte table in LDS, and a ray's miss hops

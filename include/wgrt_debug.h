@@ -40,7 +40,10 @@ struct wgrt_debug_opts {
     int fail_after_trace;
     /* Fused launches: hand-off wait bound in s_memrealtime ticks (100 MHz); 0 = the default
      * derived from num_iter.  A tiny bound makes waiting traces give up
-     * (counted in wgrt_trace_stats.handoff_giveups). */
+     * (counted in wgrt_trace_stats.handoff_giveups).  Without it, a trace is given up only once the
+     * default bound has passed AND the waiting wave has run 4096 passes since the wait began (a wave
+     * that was descheduled does not give up a correct hand-off); a given-up ray is marked abandoned,
+     * so its later traces in the call skip it instead of waiting again. */
     uint64_t handoff_wait_ticks;
 };
 

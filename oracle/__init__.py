@@ -105,6 +105,10 @@ class OracleScene:
                  eff_reg_FOV_range, luts: dict, lut_TIR, lut_gap, f32_mask: int = 0):
         """``f32_mask``: bit k set = LUT k (ic1, ic2, ic3, fc1, fc2, oc1, oc2) is complex64 in the
         reference's run, whose compiled kernel takes the cosine of its float32 angles in float32."""
+        if f32_mask not in (0, 0x7F):
+            # a mixed set: numba's unified complex128 theta would need a second cosine per table (the
+            # carried cos(theta.real) in double, the numerator in float32); the product rejects it too
+            raise ValueError("f32_mask must be 0 or 0x7f (a mixed-precision LUT set is not modelled)")
         c = lambda a, dt=np.float64: np.ascontiguousarray(a, dtype=dt)
         # single-wavelength LUT shapes (GRTF:419-427): lut_TIR [NX, NY, 4], ... -> lambda axis of 1
         self.single_lambda = np.ndim(lut_TIR) == 3

@@ -155,6 +155,16 @@ def test_c5_matches_oracle_on_blocks(dev):
     _record("C5_blocks_vs_oracle", {"blocks": len(sample), "gpu_bounces": bounces, "replayed": replayed})
 
 
+def test_c5d_matches_oracle_on_blocks(dev):
+    """C5d: the C5 batch (41x41x3x16384, stress LUT) on the design geometry (unscaled hops, CC:140) in
+    one GPU launch; 1 % of its blocks traced by the oracle."""
+    nblk = 41 * 41 * 3
+    sample = np.unique(np.linspace(0, nblk - 1, 51).astype(int))
+    bounces, replayed = _blocks_vs_oracle(dev, 41, 41, [0, 1, 2], 16384, sample, profile="stress")
+    assert bounces > 5 * 82_624_512
+    _record("C5d_blocks_vs_oracle", {"blocks": len(sample), "gpu_bounces": bounces, "replayed": replayed})
+
+
 def test_main_default_job_matches_oracle_on_blocks(dev):
     """The reference's default job (100x75 FoV x 3 lambda x 5000 rays, MAIN:16-17, 60-61) in one
     GPU launch; 5 of its 22,500 blocks traced by the oracle."""

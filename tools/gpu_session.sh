@@ -4,7 +4,7 @@
 # the first step that ends abnormally (fault / abort / timeout: exit status > 1); a plain test
 # failure (pytest exit 1) is recorded and the later steps still run.
 #   STEPS=pytest,smoke,bench,prof,traffic,pmc,configs,emulate,rehearsal  PYTEST_ARGS=...  BENCH_ARGS=...  TAG=r03
-#   configs: bench lines of C2 / C4 / C5; emulate: --emulate-ranks 2/4/8 (C3) and 8 (C4); rehearsal:
+#   configs: bench lines of C2 / C4 / C5 / C5d; emulate: --emulate-ranks 2/4/8 (C3) and 8 (C4); rehearsal:
 #   torchrun 2 ranks on the one GPU over gloo (the N > 1 code path: interleaved shards + gather)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
@@ -46,7 +46,7 @@ if [[ $STEPS == *pmc* ]]; then
     >> "$OUT/${TAG}_pmc.log" 2>&1
 fi
 if [[ $STEPS == *configs* ]]; then
-  for c in C2 C4 C5; do
+  for c in C2 C4 C5 C5d; do
     timeout -k 10 600 python bench.py --config $c --steps 10 --warmup 2 > "$OUT/${TAG}_bench_$c.log" 2>&1
     ok_or_stop $? bench_$c
   done
