@@ -605,10 +605,16 @@ __device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int
 struct JRay {
     double x, y;
     double er, ei, mr, mi;   // Jones vector (Ete, Etm), up to a global phase
-    double cos_t, ener;
+    double cos_t, ener;      // cos_t: the next interaction's denominator (cos of the ic1 angle before the first)
     double eerr;             // relative error bound of ener (threshold > 0 kernels only)
-    double gx, gy;           // miss-hop move of the current region
-    double hr, hi;           // miss-hop phase step e^{2 i lut_TIR} of the current region, applied at each hop
+    // the current coupler's two branch moves (a, b) -- in-coupler lut_gap[0:2] / [4:6], folding coupler
+    // [0:2] / [2:4], out-coupler [2:4] / [6:8] (GRTF:878, 894, 1027, 1040, 1134, 1147) -- which are also the
+    // miss hops of R2 (a), R3 (b) and R4 (a), and those miss hops' phase steps e^{2 i lut_TIR}: R2 (a)
+    // lut_TIR[0], R3 (b) and R4 (a) lut_TIR[1].  Carried from one coupler change to the next (ray start,
+    // in-coupler -> R2, R3 -> R4), so an interaction loads neither its moves nor its hop phasor.
+    double max, may, mbx, mby;
+    double har, hai, hbr, hbi;
+    float G;                 // the tile's phase-growth factor of the certification bound (kJGrowth, rounded up)
     uint32_t s;
     int region;
 };
@@ -691,11 +697,17 @@ __device__ __forceinline__ void prep_staged(const TraceArgs &A, LdsU32 *S, int j
 
 // A lane's ray from slot j of a prepared chunk.  Fused launches pass the ray's hand-off granule
 // address: it is loaded with the slot.  False: a bad ray (not traced).
-__device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t i, JLane &L,
-                                                 const uint64_t *granule = nullptr, uint64_t *gword = nullptr) {
+__device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t i, JLane &L, const double *jtiles,
+                                                 int jtile_d, const uint64_t *granule = nullptr,
+                                                 uint64_t *gword = nullptr) {
     const uint32_t tix = S[2 * 64 + j];
     L.i = (uint32_t)i;
     L.tix = tix == kBadTix ? 0u : tix;
+    // the tile header the in-coupling interaction and the in-coupler states use: cos of the ic1 angle
+    // (the first denominator), the growth factor, and the in-coupler's two branch moves
+    const double *T = jtiles + (size_t)L.tix * (size_t)jtile_d;
+    const double2 cg = *(const double2 *)(T + kJCosIc1);
+    const double2 ga = *(const double2 *)(T + kJGap + 0), gb = *(const double2 *)(T + kJGap + 4);
     L.r.x = (double)__uint_as_float(S[0 * 64 + j]);
     L.r.y = (double)__uint_as_float(S[1 * 64 + j]);
     L.r.er = (double)__uint_as_float(S[5 * 64 + j]);
@@ -704,12 +716,16 @@ __device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t
     L.r.mi = __longlong_as_double((long long)(((uint64_t)S[7 * 64 + j] << 32) | S[6 * 64 + j]));
     L.r.s = S[8 * 64 + j];
     if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.r.cos_t = 1.0;
+    L.r.cos_t = cg.x;
+    L.r.G = __double2float_ru(cg.y);
+    L.r.max = ga.x;
+    L.r.may = ga.y;
+    L.r.mbx = gb.x;
+    L.r.mby = gb.y;
+    L.r.har = L.r.hbr = 1.0;
+    L.r.hai = L.r.hbi = 0.0;
     L.r.ener = 1.0;
     L.r.eerr = 0.0;
-    L.r.gx = L.r.gy = 0.0;
-    L.r.hr = 1.0;
-    L.r.hi = 0.0;
     L.r.region = 0;
     L.bounces = 1;
     // L.pf is not set: the first pass runs the in-coupling interaction, which loads it (and a
@@ -880,23 +896,17 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const bool three = kind >= 3;
     const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
     const double t = SINGLE ? A.threshold : 0.0;
-    // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
-    // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
-    const int ga = kind >= 3 ? 2 : 0;
-    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double4 cw = block_cw(B);
-    // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
-    // issued together with its matrix, one memory round trip per interaction less
-    const double2 mva = *(const double2 *)(T + kJGap + ga);
-    const double2 mvb = *(const double2 *)(T + kJGap + gb);
-    const double denom = entry ? cg.x : r.cos_t;
+    // the moves of branch a and b of this state (GRTF:878, 894, 1027, 1040, 1134, 1147, ...) are the
+    // coupler's pair the lane carries (JRay::max ...): the taken branch's new cell word is issued together
+    // with its matrix, and neither move is loaded here
+    const double denom = r.cos_t;   // cos of the ic1 angle at the in-coupling event (lane_load_staged)
     const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka((int64_t)L.i); });
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double base = fma(nb * nb, (double)r.G, 1.0) * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
@@ -914,13 +924,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     // 0: below), issued together with the load of its double-precision matrix.  Only the taken
     // branch's cell word: loading both candidates' before the decision hid no more latency and
     // doubled the cell-word gathers (random 4-B reads of a 71 MB grid): 9-12 % slower on C3
-    const double2 mv = ba ? mva : mvb;
-    r.x = r.x + mv.x;
-    r.y = r.y + mv.y;
+    r.x = r.x + (ba ? r.max : r.mbx);
+    r.y = r.y + (ba ? r.may : r.mby);
     L.pf = locate_c(loc, r.x, r.y);
-    // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
-    // in-coupler states and R5 never hop), loaded with the taken branch's matrix
-    const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
@@ -936,12 +942,20 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     if (SINGLE) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
-    r.gx = mv.x;
-    r.gy = mv.y;
-    r.hr = hop.x;
-    r.hi = hop.y;
     if (kind == 0) {
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
+        if (ba & !in_ic) {
+            // in-coupler -> R2: the folding coupler's pair -- its move a is the in-coupler's (lut_gap[0:2]);
+            // move b lut_gap[2:4]; the phase steps of R2's and R3's miss hops, 2 lut_TIR[0] and 2 lut_TIR[1]
+            const double2 g1 = *(const double2 *)(T + kJGap + 2);
+            const double4 h = *(const double4 *)(T + kJHop);
+            r.mbx = g1.x;
+            r.mby = g1.y;
+            r.har = h.x;
+            r.hai = h.y;
+            r.hbr = h.z;
+            r.hbi = h.w;
+        }
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -1045,6 +1059,17 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, const
         L.bounces += over ? 0u : 1u;
         kind = ic ? 0 : region - 1;
         r.region = sw ? 4 : region;
+        if (sw) {
+            // R3 -> R4: the out-coupler's pair -- move a lut_gap[2:4] (the folding coupler's b) with R4's miss-hop
+            // step 2 lut_TIR[1] (R3's), move b lut_gap[6:8] (R5 never hops)
+            const double2 g3 = *(const double2 *)(KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d + kJGap + 6);
+            r.max = r.mbx;
+            r.may = r.mby;
+            r.har = r.hbr;
+            r.hai = r.hbi;
+            r.mbx = g3.x;
+            r.mby = g3.y;
+        }
         if (!hop) {
             // the switch keeps the position and its cell word: with hop runs, evaluate R4 on it now
             if (RUNS && (sw & (C.shift > 0))) continue;
@@ -1055,12 +1080,16 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, const
         // max(hops) iterations over a wave's lanes (+3 % single launch, +5 % fused on C3)
         uint32_t b = kCoarseMixed;
         int ix, iy;
+        // the region's miss hop: R2 and R4 the pair's a, R3 its b
+        const bool ua = region != 3;
+        const double gx = ua ? r.max : r.mbx, gy = ua ? r.may : r.mby;
+        const double hr = ua ? r.har : r.hbr, hi = ua ? r.hai : r.hbi;
         for (int hops = 0;; ++hops) {
-            r.x = r.x + r.gx;
-            r.y = r.y + r.gy;
+            r.x = r.x + gx;
+            r.y = r.y + gy;
             const double mr = r.mr;
-            r.mr = fma(mr, r.hr, -r.mi * r.hi);
-            r.mi = fma(mr, r.hi, r.mi * r.hr);
+            r.mr = fma(mr, hr, -r.mi * hi);
+            r.mi = fma(mr, hi, r.mi * hr);
             // the landing cell (locate_c's clamped index: the grid has a border of all-OUT cells)
             ix = min(max((int)((r.x - loc.x0) * loc.inv_h), 0), loc.ncx - 1);
             iy = min(max((int)((r.y - loc.y0) * loc.inv_h), 0), loc.ncy - 1);

@@ -304,7 +304,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         const uint32_t oc = L.i - sbase;
         const bool in_cur = oc < 64u;
         const bool ok = lane_load_staged(sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
-                                         (int)(in_cur ? oc : L.i - sbase_prev), L.i, L,
+                                         (int)(in_cur ? oc : L.i - sbase_prev), L.i, L, KA(jtiles), A.jtile_d,
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
         waiting = false;
         active = false;
