@@ -22,7 +22,7 @@ EXPORTED = ("wgrt_scene_create", "wgrt_scene_create_ex", "wgrt_scene_destroy", "
             "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify",
             "wgrt_locator_classify_host", "wgrt_selftest_math", "wgrt_status_string", "wgrt_last_error",
             "wgrt_abi_version")
-EXPORTED_DEBUG = ("wgrt_debug_shadow", "wgrt_debug_scene_copy", "wgrt_debug_coarse_host")
+EXPORTED_DEBUG = ("wgrt_debug_shadow", "wgrt_debug_scene_copy")
 
 
 class WgrtError(RuntimeError):
@@ -84,8 +84,7 @@ LUT_ORDER = ("lut_ic1", "lut_ic2", "lut_ic3", "lut_fc1", "lut_fc2", "lut_oc1", "
 
 
 class SceneOpts(ctypes.Structure):
-    _fields_ = [("cell_mm", ctypes.c_double), ("host_build", ctypes.c_int), ("lut_f32_angles", ctypes.c_int),
-                ("coarse_shift", ctypes.c_int)]
+    _fields_ = [("cell_mm", ctypes.c_double), ("host_build", ctypes.c_int), ("lut_f32_angles", ctypes.c_int)]
 
 
 class ShadowStats(ctypes.Structure):
@@ -101,9 +100,7 @@ class SceneInfo(ctypes.Structure):
                 ("grid_cells_x", ctypes.c_int64), ("grid_cells_y", ctypes.c_int64),
                 ("grid_cell_mm", ctypes.c_double), ("grid_edge_cells", ctypes.c_int64),
                 ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("jtile_bytes", ctypes.c_int64), ("coarse_shift", ctypes.c_int32), ("coarse_palette", ctypes.c_int32),
-                ("coarse_blocks_x", ctypes.c_int64), ("coarse_blocks_y", ctypes.c_int64),
-                ("coarse_uniform", ctypes.c_int64)]
+                ("jtile_bytes", ctypes.c_int64)]
 
 
 _lib = None
@@ -161,9 +158,6 @@ def load(path: str = LIB_PATH):
                                     _vp, _vp, _vp]
     L.wgrt_debug_scene_copy.restype = st
     L.wgrt_debug_scene_copy.argtypes = [_vp, ctypes.c_int, _vp, ctypes.c_int64]
-    L.wgrt_debug_coarse_host.restype = st
-    L.wgrt_debug_coarse_host.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_double, ctypes.c_int, _vp, ctypes.c_int64,
-                                         _vp, ctypes.POINTER(ctypes.c_int32), _i64, _i64, _d]
     L.wgrt_status_string.restype = ctypes.c_char_p
     L.wgrt_status_string.argtypes = [ctypes.c_int]
     L.wgrt_last_error.restype = ctypes.c_char_p
@@ -254,10 +248,9 @@ class Scene:
     def __init__(self, IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV,
                  eff_reg_FOV_range, lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2, lut_oc1, lut_oc2,
                  lut_TIR, lut_gap, device: int = 0, cell_mm: float = 0.0, host_build: bool = False,
-                 lut_f32_angles: int | None = None, coarse_shift: int = 0):
-        """``cell_mm`` / ``host_build`` / ``lut_f32_angles`` / ``coarse_shift``: wgrt_scene_opts (0 / False:
-        the defaults; ``lut_f32_angles=None``: bit k set for each LUT given in single precision,
-        luts.lut_f32_mask; ``coarse_shift=-1``: no hop runs)."""
+                 lut_f32_angles: int | None = None):
+        """``cell_mm`` / ``host_build`` / ``lut_f32_angles``: wgrt_scene_opts (0 / False: the defaults;
+        ``lut_f32_angles=None``: bit k set for each LUT given in single precision, luts.lut_f32_mask)."""
         L = load()
         desc, _keep, (nl, nx, ny, nfc, noc) = make_desc(
             IC, FC, FC_offset, OC, OC_offset, n_g, eff_reg1, eff_reg2, eff_reg_FOV, eff_reg_FOV_range,
@@ -267,7 +260,7 @@ class Scene:
             from .luts import lut_f32_mask
             lut_f32_angles = lut_f32_mask(dict(zip(LUT_ORDER, (lut_ic1, lut_ic2, lut_ic3, lut_fc1, lut_fc2,
                                                                lut_oc1, lut_oc2))))
-        opts = SceneOpts(float(cell_mm), 1 if host_build else 0, int(lut_f32_angles), int(coarse_shift))
+        opts = SceneOpts(float(cell_mm), 1 if host_build else 0, int(lut_f32_angles))
         self.lut_f32_angles = int(lut_f32_angles)
         check(L.wgrt_scene_create_ex(ctypes.byref(desc), int(device), ctypes.byref(opts), ctypes.byref(h)),
               "wgrt_scene_create")
@@ -305,22 +298,14 @@ class Scene:
 
     def debug_copy(self, which: str) -> np.ndarray:
         """Host copy of a device structure (wgrt_debug_scene_copy): "cells" (uint64 [ncy, ncx]),
-        "tiles" / "jtiles" (float64 [tiles, doubles per tile]), "coarse" (uint8 [blocks_y, blocks_x], the
-        hop runs' byte table) and "coarse_pal" (uint64 [32])."""
+        "tiles" / "jtiles" (float64 [tiles, doubles per tile])."""
         inf = self.info()
         if which == "cells":
             out = np.empty((inf["grid_cells_y"], inf["grid_cells_x"]), np.uint64)
-        elif which == "coarse":
-            nb = inf["coarse_blocks_x"] * inf["coarse_blocks_y"]
-            raw = np.empty((nb + 3) // 4 * 4, np.uint8)
-            check(load().wgrt_debug_scene_copy(self.handle, 3, raw.ctypes.data, raw.nbytes), "wgrt_debug_scene_copy")
-            return raw[:nb].reshape(inf["coarse_blocks_y"], inf["coarse_blocks_x"])
-        elif which == "coarse_pal":
-            out = np.empty(32 if inf["coarse_shift"] else 0, np.uint64)
         else:
             per = inf["tile_bytes" if which == "tiles" else "jtile_bytes"] // 8
             out = np.empty((inf["tiles"], per), np.float64)
-        k = {"cells": 0, "tiles": 1, "jtiles": 2, "coarse_pal": 4}[which]
+        k = {"cells": 0, "tiles": 1, "jtiles": 2}[which]
         check(load().wgrt_debug_scene_copy(self.handle, k, out.ctypes.data, out.nbytes), "wgrt_debug_scene_copy")
         return out
 
@@ -357,27 +342,3 @@ def locator_classify_host(geom, luts, xy: np.ndarray, cell_mm: float = 0.125) ->
           "wgrt_locator_classify_host")
     return out
 
-
-def coarse_table_host(geom, luts, cell_mm: float = 0.0, coarse_shift: int = 0):
-    """Host build of the hop runs' coarse locator (``wgrt_debug_coarse_host``; no GPU): returns
-    ``(shift, bytes uint8 [blocks_y, blocks_x], palette uint64 [32], grid)`` with grid = (x0, y0, cell mm,
-    cells_x, cells_y) of the locator -- shift 0 (off) gives empty arrays.  The same table
-    ``Scene(..., coarse_shift=...)`` builds on the device."""
-    L = load()
-    desc, keep, _ = make_desc(geom.IC, geom.FC, geom.FC_offset, geom.OC, geom.OC_offset, geom.n_g,
-                              geom.eff_reg1, geom.eff_reg2, geom.eff_reg_FOV, geom.eff_reg_FOV_range,
-                              luts["lut_ic1"], luts["lut_ic2"], luts["lut_ic3"], luts["lut_fc1"],
-                              luts["lut_fc2"], luts["lut_oc1"], luts["lut_oc2"], geom.lut_TIR, geom.lut_gap)
-    sh, bx, by = ctypes.c_int32(), ctypes.c_int64(), ctypes.c_int64()
-    grid = np.zeros(5, np.float64)
-    check(L.wgrt_debug_coarse_host(ctypes.byref(desc), float(cell_mm), int(coarse_shift), None, 0, None,
-                                   ctypes.byref(sh), ctypes.byref(bx), ctypes.byref(by), _ptr(grid)),
-          "wgrt_debug_coarse_host")
-    if sh.value == 0:
-        return 0, np.zeros((0, 0), np.uint8), np.zeros(0, np.uint64), tuple(grid)
-    tab = np.empty((by.value, bx.value), np.uint8)
-    pal = np.empty(32, np.uint64)
-    check(L.wgrt_debug_coarse_host(ctypes.byref(desc), float(cell_mm), int(coarse_shift), tab.ctypes.data_as(_vp),
-                                   tab.size, pal.ctypes.data_as(_vp), ctypes.byref(sh), ctypes.byref(bx),
-                                   ctypes.byref(by), None), "wgrt_debug_coarse_host")
-    return sh.value, tab, pal, tuple(grid)

@@ -177,9 +177,6 @@ WGRT_HD bool inside_or_on_edge_subset(double px, double py, const double *xy, in
     return inside;
 }
 
-// A locator cell word holds an EDGE class (2 bits per polygon: 0 OUT, 1 IN, 2 EDGE).
-WGRT_HD bool coarse_has_edge(uint64_t w) { return ((w >> 1) & ~w & 0x5555555555555555ull) != 0ull; }
-
 // xorshift32 (13, 17, 5) of GRTF:25-34.  gid() returns the GLOBAL ray index; it is evaluated
 // only for the zero-state fix-up (GRTF:28-29), so a kernel may look it up lazily.
 template <class GidFn>

@@ -78,26 +78,9 @@ struct TraceArgs {
     // global ray ids of an interleaved shard (wgrt_launch_opts.gid_blocks): NULL = gid_offset + i
     const int64_t *gid_blocks;
     int64_t gid_block_rays;
-    // hop runs of the Jones-vector variants (wgrt_scene_opts.coarse_shift; coarse_shift 0 = off): the
-    // coarse locator's byte table (coarse_words 32-bit words, staged into LDS by every workgroup) and
-    // its palette of cell words
-    const uint32_t *coarse;
-    const uint64_t *coarse_pal;
-    int coarse_shift, coarse_nx, coarse_words;
 };
 
-// The coarse locator of the hop runs.  A block of 2^shift x 2^shift locator cells gets one byte:
-// kCoarseMixed when its cells do not all hold one cell word without an EDGE class, else that
-// word's palette index (bits 0-4) and, in bit 3 + R for R = 2, 3, 4, whether a miss hop of region
-// R continues at any point of the block (eff_reg1 IN, none of the region's slices IN, and for R3
-// eff_reg2 IN: advance() below then hops again).  The cells' IN / OUT classes are exact for every
-// point of their cell (wgrt_scene_build.cpp), so a uniform block's word is exact for every point of
-// the block, and a block index derived from a point's cell index (cell >> shift) is consistent with
-// the cell lookup by construction.
-constexpr int kCoarseMaxBytes = 18432;   // LDS budget of the byte table (per workgroup)
-constexpr int kCoarsePal = 31;           // palette entries (index 31 unused: 0xff stays free)
-constexpr uint32_t kCoarseMixed = 0xffu;
-constexpr int kPartWords = 8;            // counter partial slot of a trace workgroup (64-bit words)
+constexpr int kPartWords = 8;   // counter partial slot of a trace workgroup (64-bit words)
 
 // A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
 // used (a volatile scalar load, a scalar-cache hit) instead of being held in an SGPR for the
@@ -605,16 +588,10 @@ __device__ __forceinline__ bool eyebox_add(const TraceArgs &A, int l, int m, int
 struct JRay {
     double x, y;
     double er, ei, mr, mi;   // Jones vector (Ete, Etm), up to a global phase
-    double cos_t, ener;      // cos_t: the next interaction's denominator (cos of the ic1 angle before the first)
+    double cos_t, ener;
     double eerr;             // relative error bound of ener (threshold > 0 kernels only)
-    // the current coupler's two branch moves (a, b) -- in-coupler lut_gap[0:2] / [4:6], folding coupler
-    // [0:2] / [2:4], out-coupler [2:4] / [6:8] (GRTF:878, 894, 1027, 1040, 1134, 1147) -- which are also the
-    // miss hops of R2 (a), R3 (b) and R4 (a), and those miss hops' phase steps e^{2 i lut_TIR}: R2 (a)
-    // lut_TIR[0], R3 (b) and R4 (a) lut_TIR[1].  Carried from one coupler change to the next (ray start,
-    // in-coupler -> R2, R3 -> R4), so an interaction loads neither its moves nor its hop phasor.
-    double max, may, mbx, mby;
-    double har, hai, hbr, hbi;
-    float G;                 // the tile's phase-growth factor of the certification bound (kJGrowth, rounded up)
+    double gx, gy;           // miss-hop move of the current region
+    double hr, hi;           // miss-hop phase step e^{2 i lut_TIR} of the current region, applied at each hop
     uint32_t s;
     int region;
 };
@@ -697,17 +674,11 @@ __device__ __forceinline__ void prep_staged(const TraceArgs &A, LdsU32 *S, int j
 
 // A lane's ray from slot j of a prepared chunk.  Fused launches pass the ray's hand-off granule
 // address: it is loaded with the slot.  False: a bad ray (not traced).
-__device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t i, JLane &L, const double *jtiles,
-                                                 int jtile_d, const uint64_t *granule = nullptr,
-                                                 uint64_t *gword = nullptr) {
+__device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t i, JLane &L,
+                                                 const uint64_t *granule = nullptr, uint64_t *gword = nullptr) {
     const uint32_t tix = S[2 * 64 + j];
     L.i = (uint32_t)i;
     L.tix = tix == kBadTix ? 0u : tix;
-    // the tile header the in-coupling interaction and the in-coupler states use: cos of the ic1 angle
-    // (the first denominator), the growth factor, and the in-coupler's two branch moves
-    const double *T = jtiles + (size_t)L.tix * (size_t)jtile_d;
-    const double2 cg = *(const double2 *)(T + kJCosIc1);
-    const double2 ga = *(const double2 *)(T + kJGap + 0), gb = *(const double2 *)(T + kJGap + 4);
     L.r.x = (double)__uint_as_float(S[0 * 64 + j]);
     L.r.y = (double)__uint_as_float(S[1 * 64 + j]);
     L.r.er = (double)__uint_as_float(S[5 * 64 + j]);
@@ -716,16 +687,12 @@ __device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t
     L.r.mi = __longlong_as_double((long long)(((uint64_t)S[7 * 64 + j] << 32) | S[6 * 64 + j]));
     L.r.s = S[8 * 64 + j];
     if (granule) *gword = __hip_atomic_load(granule, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    L.r.cos_t = cg.x;
-    L.r.G = __double2float_ru(cg.y);
-    L.r.max = ga.x;
-    L.r.may = ga.y;
-    L.r.mbx = gb.x;
-    L.r.mby = gb.y;
-    L.r.har = L.r.hbr = 1.0;
-    L.r.hai = L.r.hbi = 0.0;
+    L.r.cos_t = 1.0;
     L.r.ener = 1.0;
     L.r.eerr = 0.0;
+    L.r.gx = L.r.gy = 0.0;
+    L.r.hr = 1.0;
+    L.r.hi = 0.0;
     L.r.region = 0;
     L.bounces = 1;
     // L.pf is not set: the first pass runs the in-coupling interaction, which loads it (and a
@@ -896,17 +863,23 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const bool three = kind >= 3;
     const bool thr = kind >= 1;   // the ener > threshold guard exists only in R2..R5
     const double t = SINGLE ? A.threshold : 0.0;
+    // the moves of branch a (index 0) and b (index 1) of this state (GRTF:878, 894, 1027, 1040,
+    // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
+    const int ga = kind >= 3 ? 2 : 0;
+    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
+    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double4 cw = block_cw(B);
-    // the moves of branch a and b of this state (GRTF:878, 894, 1027, 1040, 1134, 1147, ...) are the
-    // coupler's pair the lane carries (JRay::max ...): the taken branch's new cell word is issued together
-    // with its matrix, and neither move is loaded here
-    const double denom = r.cos_t;   // cos of the ic1 angle at the in-coupling event (lane_load_staged)
+    // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
+    // issued together with its matrix, one memory round trip per interaction less
+    const double2 mva = *(const double2 *)(T + kJGap + ga);
+    const double2 mvb = *(const double2 *)(T + kJGap + gb);
+    const double denom = entry ? cg.x : r.cos_t;
     const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka((int64_t)L.i); });
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double base = fma(nb * nb, (double)r.G, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
@@ -924,9 +897,13 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     // 0: below), issued together with the load of its double-precision matrix.  Only the taken
     // branch's cell word: loading both candidates' before the decision hid no more latency and
     // doubled the cell-word gathers (random 4-B reads of a 71 MB grid): 9-12 % slower on C3
-    r.x = r.x + (ba ? r.max : r.mbx);
-    r.y = r.y + (ba ? r.may : r.mby);
+    const double2 mv = ba ? mva : mvb;
+    r.x = r.x + mv.x;
+    r.y = r.y + mv.y;
     L.pf = locate_c(loc, r.x, r.y);
+    // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
+    // in-coupler states and R5 never hop), loaded with the taken branch's matrix
+    const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
@@ -942,20 +919,12 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     if (SINGLE) r.eerr += A.cert_tol * base * B[kJBlockW + b] * 1.01 * rcp_nr(ab) + 1e-15;
     r.ener = r.ener * ab;
     r.cos_t = ba ? cw.x : cw.y;
+    r.gx = mv.x;
+    r.gy = mv.y;
+    r.hr = hop.x;
+    r.hi = hop.y;
     if (kind == 0) {
         const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
-        if (ba & !in_ic) {
-            // in-coupler -> R2: the folding coupler's pair -- its move a is the in-coupler's (lut_gap[0:2]);
-            // move b lut_gap[2:4]; the phase steps of R2's and R3's miss hops, 2 lut_TIR[0] and 2 lut_TIR[1]
-            const double2 g1 = *(const double2 *)(T + kJGap + 2);
-            const double4 h = *(const double4 *)(T + kJHop);
-            r.mbx = g1.x;
-            r.mby = g1.y;
-            r.har = h.x;
-            r.hai = h.y;
-            r.hbr = h.z;
-            r.hbi = h.w;
-        }
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -991,123 +960,65 @@ __device__ __forceinline__ typename Loc::Word resolve_edges(const Loc &loc, type
 __device__ __forceinline__ int low_bit(uint32_t v) { return __builtin_ctz(v); }
 __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); }
 
-// The coarse locator's byte table and palette as staged in a workgroup's LDS (jones_body); shift 0:
-// no hop runs.
-typedef uint8_t __attribute__((address_space(3))) LdsU8;
-typedef uint64_t __attribute__((address_space(3))) LdsU64;
-struct CoarseLds {
-    const LdsU8 *b;
-    const LdsU64 *pal;
-    int shift, nx;
-};
-
-// Same contract as advance() for the Jones-vector lane: the loop iterations of GRTF:905-1246 that
-// need no Monte-Carlo interaction -- miss hops and the R3 -> R4 switch -- up to the next
-// interaction's block index (returned), a termination (kDie), or a position whose cell word must
-// come from the global locator (kTransit: its load is issued here, read by the next pass).  It
-// starts from the cell word loaded a pass earlier (JLane::pf).  The outcome is computed as selects
-// from the word's class bits (in the word's own width: 32 bits for variant 7) -- one straight-line
+// Same contract as advance() for the Jones-vector lane: one loop iteration of GRTF:905-1246 that
+// needs no Monte-Carlo interaction (a miss hop or the R3 -> R4 switch: kTransit), or the next
+// interaction's block index, or kDie.  It tests the cell word loaded a pass earlier (JLane::pf);
+// a miss hop issues the load of the next one.  The outcome is computed as selects from the cell
+// word's class bits (in the word's own width: 32 bits for variant 7) -- one straight-line
 // evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
-//
-// Hop runs (C.shift > 0): a miss hop that lands in a uniform block of the coarse
-// locator knows its new cell word without a memory access -- the block's byte says whether the
-// region's miss hop continues there, and its palette word is the cell word -- so the lane keeps
-// hopping (each hop one bounce, the same float64 additions as one hop per pass) and evaluates the
-// word it lands on in the same pass; an R3 -> R4 switch is evaluated on, at the same position, too.
-// Only a landing in a mixed block ends the pass with a global cell-word load.
-#ifndef WGRT_HOP_MAX
-#define WGRT_HOP_MAX 1000000
-#endif
-template <bool RUNS, class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, const CoarseLds &C, JLane &L, int &kind) {
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
     constexpr W kTop = (W)1 << (kBits - 1);
     JRay &r = L.r;
     W c = (W)L.pf;
+    const int region = r.region;
     const int nfc = A.nfc, noc = A.noc;
-    for (;;) {
-        const int region = r.region;
-        // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
-        const bool fc = region <= 3;
-        const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
-        const W gmask = 2 * count < kBits ? ((W)1 << (2 * count)) - (W)1 : (W)~(W)0;
-        W f = (c >> (2 * first)) & gmask;
-        W in = f & kLow, cand = in | ((f >> 1) & kLow);
-        const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
-        const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
-        const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
-        if (e1edge | sedge | e2edge) {   // never for a palette word (no EDGE class)
-            c = resolve_edges(loc, c, region, first, count, r.x, r.y);
-            f = (c >> (2 * first)) & gmask;
-            in = f & kLow;
-            cand = in | ((f >> 1) & kLow);
-        }
-        const bool over = L.bounces > (uint32_t)kMaxLoop;   // range(1e5) exhausted (GRTF:905)
-        const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
-        const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
-        const bool ic = region <= 1;
-        const bool hit = !ic & (cand != 0);
-        const int sl = low_bit((W)(cand | kTop)) >> 1;
-        const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
-        const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
-        const bool hop = !die & !ic & !hit & !sw;                               // miss hop
-        const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
-        L.bounces += over ? 0u : 1u;
-        kind = ic ? 0 : region - 1;
-        r.region = sw ? 4 : region;
-        if (sw) {
-            // R3 -> R4: the out-coupler's pair -- move a lut_gap[2:4] (the folding coupler's b) with R4's miss-hop
-            // step 2 lut_TIR[1] (R3's), move b lut_gap[6:8] (R5 never hops)
-            const double2 g3 = *(const double2 *)(KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d + kJGap + 6);
-            r.max = r.mbx;
-            r.may = r.mby;
-            r.har = r.hbr;
-            r.hai = r.hbi;
-            r.mbx = g3.x;
-            r.mby = g3.y;
-        }
-        if (!hop) {
-            // the switch keeps the position and its cell word: with hop runs, evaluate R4 on it now
-            if (RUNS && (sw & (C.shift > 0))) continue;
-            return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
-        }
-        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178); delta_phase += 2 lut_TIR (GRTF:1052,
-        // 1108, 1178) as a turn of Etm at the hop itself: a deferred per-interaction loop ran
-        // max(hops) iterations over a wave's lanes (+3 % single launch, +5 % fused on C3)
-        uint32_t b = kCoarseMixed;
-        int ix, iy;
-        // the region's miss hop: R2 and R4 the pair's a, R3 its b
-        const bool ua = region != 3;
-        const double gx = ua ? r.max : r.mbx, gy = ua ? r.may : r.mby;
-        const double hr = ua ? r.har : r.hbr, hi = ua ? r.hai : r.hbi;
-        for (int hops = 0;; ++hops) {
-            r.x = r.x + gx;
-            r.y = r.y + gy;
-            const double mr = r.mr;
-            r.mr = fma(mr, hr, -r.mi * hi);
-            r.mi = fma(mr, hi, r.mi * hr);
-            // the landing cell (locate_c's clamped index: the grid has a border of all-OUT cells)
-            ix = min(max((int)((r.x - loc.x0) * loc.inv_h), 0), loc.ncx - 1);
-            iy = min(max((int)((r.y - loc.y0) * loc.inv_h), 0), loc.ncy - 1);
-            if (!RUNS || C.shift == 0) break;
-            b = C.b[(iy >> C.shift) * C.nx + (ix >> C.shift)];
-            if (hops >= WGRT_HOP_MAX) break;
-            // the region's miss hop continues in this block (bit 3 + region; never in a mixed block,
-            // and the loop cap is the evaluation's own test)
-            if (!(((b >> (3 + region)) & 1u) & (b != kCoarseMixed) & (L.bounces <= (uint32_t)kMaxLoop))) break;
-            ++L.bounces;
-        }
-        if (b == kCoarseMixed) {
-            L.pf = loc.cells[iy * loc.ncx + ix];   // read by the next pass
-            return kTransit;
-        }
-        c = (W)C.pal[b & 31u];
-        L.pf = c;
+    // the coupler slices this region scans (GRTF:1002-1005, 1112-1115) and its blocks
+    const bool fc = region <= 3;
+    const int first = fc ? kPolyFC0 : kPolyFC0 + nfc, count = fc ? nfc : noc;
+    const W gmask = 2 * count < kBits ? ((W)1 << (2 * count)) - (W)1 : (W)~(W)0;
+    W f = (c >> (2 * first)) & gmask;
+    W in = f & kLow, cand = in | ((f >> 1) & kLow);
+    const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
+    const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
+    const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
+    if (e1edge | sedge | e2edge) {
+        c = resolve_edges(loc, c, region, first, count, r.x, r.y);
+        f = (c >> (2 * first)) & gmask;
+        in = f & kLow;
+        cand = in | ((f >> 1) & kLow);
     }
+    const bool over = L.bounces > (uint32_t)kMaxLoop;   // range(1e5) exhausted (GRTF:905)
+    const bool eff1 = ((c >> (2 * kPolyEff1)) & 3u) == 1u;   // GRTF:906
+    const bool eff2 = ((c >> (2 * kPolyEff2)) & 3u) == 1u;
+    const bool ic = region <= 1;
+    const bool hit = !ic & (cand != 0);
+    const int sl = low_bit((W)(cand | kTop)) >> 1;
+    const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
+    const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
+    const bool hop = !die & !ic & !hit & !sw;                               // miss hop
+    const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
+    L.bounces += over ? 0u : 1u;
+    kind = ic ? 0 : region - 1;
+    r.region = sw ? 4 : region;
+    if (hop) {
+        // miss hop (GRTF:1049-1052, 1105-1108, 1175-1178)
+        r.x = r.x + r.gx;
+        r.y = r.y + r.gy;
+        // delta_phase += 2 lut_TIR (GRTF:1052, 1108, 1178) as a turn of Etm at the hop itself: a
+        // deferred per-interaction loop ran max(hops) iterations over a wave's lanes (+3 % single
+        // launch, +5 % fused on C3, +10 % on C5's short hops)
+        const double mr = r.mr;
+        r.mr = fma(mr, r.hr, -r.mi * r.hi);
+        r.mi = fma(mr, r.hi, r.mi * r.hr);
+        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
+    }
+    return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
 }
 
 template <class LaneT>

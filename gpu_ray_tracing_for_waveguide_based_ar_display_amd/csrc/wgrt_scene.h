@@ -27,11 +27,6 @@ struct wgrt_scene {
     wgrt::LocatorHost loc_host;  // grid parameters (cells / verts vectors released after upload)
     int64_t tiles = 0;
     int64_t edge_cells = 0;        // locator cells with an EDGE class
-    // the coarse locator of the hop runs (wgrt_scene_build.h CoarseHost; coarse_shift 0 = off)
-    uint32_t *d_coarse = nullptr;
-    uint64_t *d_coarse_pal = nullptr;
-    int coarse_shift = 0, coarse_nbx = 0, coarse_nby = 0, coarse_words = 0, coarse_npal = 0;
-    int64_t coarse_uniform = 0;
     int jones_grid[2][2][2] = {};   // resident 256-thread workgroups: [64-bit cells][fused][single wavelength]
     int jones_tl_grid[2] = {};      // ... of the debug timeline instantiations (32-bit cells): [fused]
     // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so

@@ -27,7 +27,6 @@
 #include <cmath>
 #include <cstdint>
 #include <cstring>
-#include <map>
 #include <stdexcept>
 #include <string>
 #include <map>
@@ -314,75 +313,6 @@ void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys
     for (int64_t k = 0; k < d.n_oc_slices; ++k) {
         polys.push_back(d.OC + 2 * d.OC_offset[k]);
         nv.push_back(d.OC_offset[k + 1] - d.OC_offset[k]);
-    }
-}
-
-int coarse_shift_for(int requested, int ncx, int ncy) {
-    if (requested < 0 || ncx <= 0 || ncy <= 0) return 0;
-    int s = requested == 0 ? kCoarseDefaultShift : requested;
-    for (; s <= 16; ++s) {
-        const int64_t nbx = ((int64_t)(ncx - 1) >> s) + 1, nby = ((int64_t)(ncy - 1) >> s) + 1;
-        if (nbx * nby <= kCoarseTableMax) return s;
-    }
-    return 0;
-}
-
-void coarse_reduce_host(const std::vector<uint64_t> &cells, int ncx, int ncy, int shift, std::vector<uint64_t> &word,
-                        std::vector<uint8_t> &uniform) {
-    const int nbx = ((ncx - 1) >> shift) + 1, nby = ((ncy - 1) >> shift) + 1;
-    word.assign((size_t)nbx * nby, 0);
-    uniform.assign((size_t)nbx * nby, 0);
-    for (int by = 0; by < nby; ++by)
-        for (int bx = 0; bx < nbx; ++bx) {
-            const int x0 = bx << shift, y0 = by << shift;
-            const int x1 = std::min(x0 + (1 << shift), ncx), y1 = std::min(y0 + (1 << shift), ncy);
-            const uint64_t w0 = cells[(size_t)y0 * ncx + x0];
-            bool u = !coarse_has_edge(w0);
-            for (int y = y0; y < y1 && u; ++y)
-                for (int x = x0; x < x1 && u; ++x) u = cells[(size_t)y * ncx + x] == w0;
-            word[(size_t)by * nbx + bx] = w0;
-            uniform[(size_t)by * nbx + bx] = u ? 1 : 0;
-        }
-}
-
-void coarse_table(const std::vector<uint64_t> &word, const std::vector<uint8_t> &uniform, int nbx, int nby, int shift,
-                  int nfc, int noc, CoarseHost &out) {
-    out = CoarseHost{};
-    out.shift = shift;
-    out.nbx = nbx;
-    out.nby = nby;
-    const size_t nb = (size_t)nbx * nby;
-    out.bytes.assign((nb + 3) & ~(size_t)3, (uint8_t)0xff);
-    out.pal.assign(32, 0);
-    // the palette: the most frequent uniform words (ties by value, so both builds agree)
-    std::map<uint64_t, int64_t> count;
-    for (size_t k = 0; k < nb; ++k)
-        if (uniform[k]) ++count[word[k]];
-    std::vector<std::pair<int64_t, uint64_t>> order;
-    for (const auto &kv : count) order.push_back({-kv.second, kv.first});
-    std::sort(order.begin(), order.end());
-    std::map<uint64_t, int> index;
-    for (const auto &e : order) {
-        if ((int)index.size() == 31) break;
-        out.pal[index.size()] = e.second;
-        index[e.second] = (int)index.size();
-    }
-    out.npal = (int)index.size();
-    auto cls = [](uint64_t w, int k) { return (unsigned)(w >> (2 * k)) & 3u; };
-    for (size_t k = 0; k < nb; ++k) {
-        if (!uniform[k]) continue;
-        const auto it = index.find(word[k]);
-        if (it == index.end()) continue;
-        const uint64_t w = word[k];
-        bool any_fc = false, any_oc = false;
-        for (int s = 0; s < nfc; ++s) any_fc |= cls(w, 3 + s) == 1u;
-        for (int s = 0; s < noc; ++s) any_oc |= cls(w, 3 + nfc + s) == 1u;
-        const bool eff1 = cls(w, 0) == 1u, eff2 = cls(w, 1) == 1u;
-        // a miss hop of region R continues at this word (wgrt_device.h advance): R2 eff_reg1 IN and
-        // no FC slice; R3 also eff_reg2 IN; R4 eff_reg1 IN and no OC slice
-        const bool f2 = eff1 && !any_fc, f3 = f2 && eff2, f4 = eff1 && !any_oc;
-        out.bytes[k] = (uint8_t)(it->second | (f2 ? 0x20 : 0) | (f3 ? 0x40 : 0) | (f4 ? 0x80 : 0));
-        ++out.uniform;
     }
 }
 

@@ -59,26 +59,5 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, 
 // the polygon list the locator covers: eff_reg1, eff_reg2, IC, FC slices, OC slices
 void scene_polygons(const wgrt_scene_desc &d, std::vector<const double *> &polys, std::vector<int64_t> &nv);
 
-// The coarse locator of the hop runs (wgrt_device.h kCoarse*): blocks of 2^shift x 2^shift cells.
-struct CoarseHost {
-    int shift = 0;                 // 0: off
-    int nbx = 0, nby = 0;
-    std::vector<uint8_t> bytes;    // [nby][nbx], padded to a multiple of 4 bytes
-    std::vector<uint64_t> pal;     // 32 entries (unused ones 0)
-    int npal = 0;
-    int64_t uniform = 0;           // blocks with a palette word
-};
-constexpr int kCoarseDefaultShift = 5;   // 1/4-mm blocks of the default 1/128-mm cells
-constexpr int kCoarseTableMax = 18432;   // = wgrt_device.h kCoarseMaxBytes
-// the block shift a request resolves to (0 default, < 0 off): coarser until the table fits
-int coarse_shift_for(int requested, int ncx, int ncy);
-// per block: its first cell's word and whether every cell of the block holds that word and it has
-// no EDGE class (the device build runs coarse_blocks_kernel, the same rule)
-void coarse_reduce_host(const std::vector<uint64_t> &cells, int ncx, int ncy, int shift, std::vector<uint64_t> &word,
-                        std::vector<uint8_t> &uniform);
-// the byte table and palette from the per-block words (npoly polygons: eff_reg1, eff_reg2, IC, nfc FC
-// slices, noc OC slices)
-void coarse_table(const std::vector<uint64_t> &word, const std::vector<uint8_t> &uniform, int nbx, int nby, int shift,
-                  int nfc, int noc, CoarseHost &out);
 
 }  // namespace wgrt

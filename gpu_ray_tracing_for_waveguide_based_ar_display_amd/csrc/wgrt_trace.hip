@@ -228,17 +228,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
-    // the coarse locator of the hop runs, staged into this workgroup's LDS (every wave of the
-    // workgroup takes part, before any of them starts its loop)
-    __shared__ uint32_t coarse_lds[kCoarseMaxBytes / 4];
-    __shared__ uint64_t coarse_pal[32];
-    CoarseLds C{(const LdsU8 *)(LdsU32 *)coarse_lds, (const LdsU64 *)coarse_pal, A.coarse_shift, A.coarse_nx};
-    if (A.coarse_shift > 0) {
-        const uint32_t *const src = KA(coarse);
-        for (int k = threadIdx.x; k < A.coarse_words; k += blockDim.x) coarse_lds[k] = src[k];
-        if (threadIdx.x < 32) coarse_pal[threadIdx.x] = KA(coarse_pal)[threadIdx.x];
-        __syncthreads();
-    }
     int head = xcc_id();
     int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
     // debug timeline (TL instantiations only): per wave, start / queue exhausted / end
@@ -304,7 +293,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         const uint32_t oc = L.i - sbase;
         const bool in_cur = oc < 64u;
         const bool ok = lane_load_staged(sbufs + (in_cur ? sb : sb ^ 1) * (kStageCols * 64),
-                                         (int)(in_cur ? oc : L.i - sbase_prev), L.i, L, KA(jtiles), A.jtile_d,
+                                         (int)(in_cur ? oc : L.i - sbase_prev), L.i, L,
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
         waiting = false;
         active = false;
@@ -404,15 +393,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
     };
 
-#ifndef WGRT_HOP_BULK
-#define WGRT_HOP_BULK 1
-#endif
-#ifndef WGRT_HOP_TAIL
-#define WGRT_HOP_TAIL 1
-#endif
     for (;;) {
         if (active) {
-            blk = advance<WGRT_HOP_BULK != 0>(A, loc, C, L, kind);
+            blk = advance(A, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
@@ -532,7 +515,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // The first pass continues the one the main loop broke off (advance and refill done).
         for (bool first = true;; first = false) {
             if (!first && active) {
-                blk = advance<WGRT_HOP_TAIL != 0>(A, loc, C, L, kind);
+                blk = advance(A, loc, L, kind);
                 entry = false;
                 if (blk == kDie) retire();
             }
@@ -750,24 +733,6 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *verts
     if ((threadIdx.x & 63) == 0 && edges) atomicAdd(edge_cells, (unsigned long long)edges);
 }
 
-// The coarse locator of the hop runs: one thread per block of 2^shift x 2^shift cells -- the block's
-// first cell word, and whether every cell of the block holds it and it has no EDGE class (the
-// host build's coarse_reduce_host rule).
-__global__ __launch_bounds__(256) void coarse_blocks_kernel(const uint64_t *cells, int ncx, int ncy, int shift, int nbx,
-                                                            int nby, uint64_t *word, uint8_t *uniform) {
-    const int64_t k = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    if (k >= (int64_t)nbx * nby) return;
-    const int bx = (int)(k % nbx), by = (int)(k / nbx);
-    const int x0 = bx << shift, y0 = by << shift;
-    const int x1 = min(x0 + (1 << shift), ncx), y1 = min(y0 + (1 << shift), ncy);
-    const uint64_t w0 = cells[(size_t)y0 * ncx + x0];
-    bool u = !coarse_has_edge(w0);
-    for (int y = y0; y < y1 && u; ++y)
-        for (int x = x0; x < x1 && u; ++x) u = cells[(size_t)y * ncx + x] == w0;
-    word[k] = w0;
-    uniform[k] = u ? 1 : 0;
-}
-
 // One thread per (lambda, m, n) tile: the exact lane's tile and its Jones-vector tile
 // (wgrt_pack.h pack_tile, the host build's code); flags any non-finite value.
 __global__ __launch_bounds__(64) void pack_tiles_kernel(PackView v, int64_t ntiles, double *tiles, double *jtiles,
@@ -952,50 +917,6 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
         s->edge_cells = (int64_t)ec;
     }
     {
-        // the coarse locator of the hop runs (from the cell words on the device, or the host's)
-        const LocatorHost &L = host.loc;
-        const int shift = coarse_shift_for(opts ? opts->coarse_shift : 0, L.ncx, L.ncy);
-        if (shift > 0) {
-            const int nbx = ((L.ncx - 1) >> shift) + 1, nby = ((L.ncy - 1) >> shift) + 1;
-            const size_t nb = (size_t)nbx * nby;
-            std::vector<uint64_t> word;
-            std::vector<uint8_t> uni;
-            if (host_build) {
-                coarse_reduce_host(L.cells, L.ncx, L.ncy, shift, word, uni);
-            } else {
-                uint64_t *dw = nullptr;
-                uint8_t *du = nullptr;
-                if ((st = alloc_n(nb, &dw)) != WGRT_OK || (st = alloc_n(nb, &du)) != WGRT_OK) {
-                    (void)hipFree(dw);
-                    return bail(st);
-                }
-                hipLaunchKernelGGL(coarse_blocks_kernel, dim3((unsigned)((nb + 255) / 256)), dim3(256), 0, 0,
-                                   s->d_cells, L.ncx, L.ncy, shift, nbx, nby, dw, du);
-                word.resize(nb);
-                uni.resize(nb);
-                hipError_t e = hipGetLastError();
-                if (e == hipSuccess) e = hipMemcpy(word.data(), dw, nb * sizeof(uint64_t), hipMemcpyDeviceToHost);
-                if (e == hipSuccess) e = hipMemcpy(uni.data(), du, nb, hipMemcpyDeviceToHost);
-                (void)hipFree(dw);
-                (void)hipFree(du);
-                if (e != hipSuccess)
-                    return bail(fail(WGRT_ERR_HIP, std::string("coarse locator: ") + hipGetErrorString(e)));
-            }
-            CoarseHost ch;
-            coarse_table(word, uni, nbx, nby, shift, s->nfc, s->noc, ch);
-            std::vector<uint32_t> words(ch.bytes.size() / 4);
-            std::memcpy(words.data(), ch.bytes.data(), ch.bytes.size());
-            if ((st = upload(words, &s->d_coarse)) != WGRT_OK || (st = upload(ch.pal, &s->d_coarse_pal)) != WGRT_OK)
-                return bail(st);
-            s->coarse_shift = shift;
-            s->coarse_nbx = nbx;
-            s->coarse_nby = nby;
-            s->coarse_words = (int)words.size();
-            s->coarse_npal = ch.npal;
-            s->coarse_uniform = ch.uniform;
-        }
-    }
-    {
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
         // resident workgroups of each instantiation (cell width x fused x single wavelength)
@@ -1042,8 +963,6 @@ wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     (void)hipFree(s->d_row_off);
     (void)hipFree(s->d_row_edges);
     (void)hipFree(s->d_bands);
-    (void)hipFree(s->d_coarse);
-    (void)hipFree(s->d_coarse_pal);
     for (auto &kv : s->scratch) {
         (void)hipFree(kv.second.ctr);
         (void)hipFree(kv.second.list);
@@ -1068,11 +987,6 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->n_polygons = s->npoly;
     info->device = s->device;
     info->jtile_bytes = (int64_t)s->jtile_d * 8;
-    info->coarse_shift = s->coarse_shift;
-    info->coarse_palette = s->coarse_npal;
-    info->coarse_blocks_x = s->coarse_nbx;
-    info->coarse_blocks_y = s->coarse_nby;
-    info->coarse_uniform = s->coarse_uniform;
     return WGRT_OK;
 }
 
@@ -1289,11 +1203,6 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
     A.n_iter = 1;
-    A.coarse = s->d_coarse;
-    A.coarse_pal = s->d_coarse_pal;
-    A.coarse_shift = s->coarse_shift;
-    A.coarse_nx = s->coarse_nbx;
-    A.coarse_words = s->coarse_words;
     hipStream_t st = (hipStream_t)stream;
     if (variant == 1) {
         const int64_t blocks = (n_rays + 255) / 256;
@@ -1561,44 +1470,6 @@ wgrt_status wgrt_locator_classify_host(const wgrt_scene_desc *desc, double cell_
     return WGRT_OK;
 }
 
-wgrt_status wgrt_debug_coarse_host(const wgrt_scene_desc *desc, double cell_mm, int coarse_shift, uint8_t *bytes_out,
-                                   int64_t bytes_cap, uint64_t *pal_out, int32_t *shift_out, int64_t *blocks_x,
-                                   int64_t *blocks_y, double *grid_out) {
-    if (!desc || !shift_out || !blocks_x || !blocks_y) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
-    if (!(cell_mm >= 0.0)) return fail(WGRT_ERR_INVALID_ARGUMENT, "cell_mm must be >= 0");
-    SceneHost host;
-    try {
-        build_scene_host(*desc, cell_mm > 0.0 ? cell_mm : kDefaultCellMm, host, true, false);
-    } catch (const std::exception &e) {
-        return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
-    }
-    const LocatorHost &L = host.loc;
-    const int shift = coarse_shift_for(coarse_shift, L.ncx, L.ncy);
-    *shift_out = shift;
-    *blocks_x = *blocks_y = 0;
-    if (grid_out) {
-        grid_out[0] = L.x0;
-        grid_out[1] = L.y0;
-        grid_out[2] = L.h;
-        grid_out[3] = L.ncx;
-        grid_out[4] = L.ncy;
-    }
-    if (shift == 0) return WGRT_OK;
-    const int nbx = ((L.ncx - 1) >> shift) + 1, nby = ((L.ncy - 1) >> shift) + 1;
-    *blocks_x = nbx;
-    *blocks_y = nby;
-    if (!bytes_out && !pal_out) return WGRT_OK;
-    if (bytes_out && bytes_cap < (int64_t)nbx * nby) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes_cap too small");
-    std::vector<uint64_t> word;
-    std::vector<uint8_t> uni;
-    coarse_reduce_host(L.cells, L.ncx, L.ncy, shift, word, uni);
-    CoarseHost ch;
-    coarse_table(word, uni, nbx, nby, shift, (int)desc->n_fc_slices, (int)desc->n_oc_slices, ch);
-    if (bytes_out) std::memcpy(bytes_out, ch.bytes.data(), (size_t)nbx * nby);
-    if (pal_out) std::memcpy(pal_out, ch.pal.data(), 32 * sizeof(uint64_t));
-    return WGRT_OK;
-}
-
 wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int64_t bytes) {
     if (!s || !dst) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / dst");
     const size_t ncells = (size_t)s->loc_host.ncx * s->loc_host.ncy;
@@ -1608,12 +1479,9 @@ wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int
         case 0: src = s->d_cells, n = ncells * sizeof(uint64_t); break;
         case 1: src = s->d_tiles, n = (size_t)s->tiles * s->tile_d * sizeof(double); break;
         case 2: src = s->d_jtiles, n = (size_t)s->tiles * s->jtile_d * sizeof(double); break;
-        case 3: src = s->d_coarse, n = (size_t)s->coarse_words * 4; break;
-        case 4: src = s->d_coarse_pal, n = s->d_coarse_pal ? 32 * sizeof(uint64_t) : 0; break;
-        default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles, 3 coarse table, 4 palette");
+        default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles");
     }
     if (bytes != (int64_t)n) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes must be " + std::to_string(n));
-    if (n == 0) return WGRT_OK;
     HIP_TRY(hipSetDevice(s->device));
     HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return WGRT_OK;

@@ -115,11 +115,6 @@ typedef struct {
     int32_t n_polygons;
     int32_t device;
     int64_t jtile_bytes;       /* Jones-vector tile per (lambda, FoV) (variants 7 / 9)  */
-    /* ABI 5: the coarse locator of the hop runs (wgrt_scene_opts.coarse_shift) */
-    int32_t coarse_shift;      /* blocks of 2^coarse_shift x 2^coarse_shift locator cells; 0 = off */
-    int32_t coarse_palette;    /* distinct cell words the uniform blocks hold (<= 31)              */
-    int64_t coarse_blocks_x, coarse_blocks_y;
-    int64_t coarse_uniform;    /* blocks answered on chip (one EDGE-free cell word in every cell)  */
 } wgrt_scene_info;
 
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon
@@ -141,12 +136,6 @@ typedef struct {
                              ABI 5: only 0 and 0x7f (all seven tables complex64) are accepted; a mixed set
                              is WGRT_ERR_UNSUPPORTED (numba would carry the ray's angle as complex128 while a
                              complex64 table's own cosine stays float32: see wgrt_scene_create_ex). */
-    int coarse_shift;     /* ABI 5.  Hop runs of the Jones-vector variants: a block of
-                             2^coarse_shift x 2^coarse_shift locator cells whose cells all hold one cell word
-                             without an EDGE class is answered from a byte table in LDS, and a ray's miss hops
-                             (GRTF:1049-1052, 1105-1108, 1175-1178) that land in such blocks run inside one
-                             pass of the wave loop.  0 = default (5: 1/4-mm blocks at the default cell), made
-                             coarser until the table fits the LDS budget; -1 = off.  Results are identical. */
 } wgrt_scene_opts;
 wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const wgrt_scene_opts *opts,
                                  wgrt_scene **out);

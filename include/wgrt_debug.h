@@ -76,22 +76,8 @@ wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, in
 
 /* Copies one of a scene's device structures to host memory dst (bytes must equal its size):
  * which = 0 the locator cell words (uint64, ncx * ncy), 1 the exact lane's tiles, 2 the
- * Jones-vector tiles (doubles, tiles * tile / jtile doubles; wgrt_scene_info), 3 the coarse
- * locator's byte table of the hop runs (coarse_blocks_x * coarse_blocks_y bytes, padded to a multiple
- * of 4), 4 its palette (32 uint64 cell words); 3 / 4 are empty (bytes 0) when the hop runs are off. */
+ * Jones-vector tiles (doubles, tiles * tile / jtile doubles; wgrt_scene_info). */
 wgrt_status wgrt_debug_scene_copy(const wgrt_scene *scene, int which, void *dst, int64_t bytes);
-
-/* Host build of the coarse locator of the hop runs (test hook, no GPU): the scene's locator with
- * cell size cell_mm (0: the default) and block shift coarse_shift (wgrt_scene_opts semantics) is
- * built on the host and reduced to its byte table and palette, exactly as wgrt_scene_create_ex does.
- * Outputs: *shift_out (0: off), *blocks_x, *blocks_y, grid_out[5] (optional: the locator grid's x0, y0,
- * cell size, cells_x, cells_y -- cell (cx, cy) = (int)((x - x0) / cell), block = cell >> shift); bytes_out (blocks_x * blocks_y bytes, row
- * major; bytes_cap must be at least that) and pal_out (32 words) may be NULL to query the sizes.  The
- * byte of a block is 0xff (mixed) or palette index | 0x20 (an R2 miss hop continues) | 0x40 (R3) |
- * 0x80 (R4). */
-wgrt_status wgrt_debug_coarse_host(const wgrt_scene_desc *desc, double cell_mm, int coarse_shift, uint8_t *bytes_out,
-                                   int64_t bytes_cap, uint64_t *pal_out, int32_t *shift_out, int64_t *blocks_x,
-                                   int64_t *blocks_y, double *grid_out);
 
 #ifdef __cplusplus
 }
