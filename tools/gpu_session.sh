@@ -32,7 +32,7 @@ if [[ $STEPS == *bench* ]]; then
 fi
 if [[ $STEPS == *prof* ]]; then
   (cd /tmp && timeout -k 10 600 rocprofv3 --kernel-trace --stats -d "$OUT/${TAG}_prof" -o run --output-format csv -- \
-    python3 "$ROOT/bench.py" --no-cpu-baseline ${BENCH_ARGS:-} > "$OUT/${TAG}_bench_prof.log" 2>&1)
+    python3 "$ROOT/bench.py" --no-cpu-baseline --no-extras ${BENCH_ARGS:-} > "$OUT/${TAG}_bench_prof.log" 2>&1)
   ok_or_stop $? prof
 fi
 if [[ $STEPS == *traffic* ]]; then
@@ -61,7 +61,7 @@ if [[ $STEPS == *emulate* ]]; then
 fi
 if [[ $STEPS == *rehearsal* ]]; then
   timeout -k 10 300 python -m torch.distributed.run --nnodes=1 --nproc-per-node 2 --master-addr 127.0.0.1 \
-    --master-port 29517 bench.py --gpus 2 --steps 10 --warmup 2 --dist-backend gloo --one-device --no-cpu-baseline \
+    --master-port 29517 bench.py --gpus 2 --steps 20 --warmup 2 --dist-backend gloo --one-device --no-cpu-baseline \
     > "$OUT/${TAG}_rehearsal_2ranks.log" 2>&1
   ok_or_stop $? rehearsal
 fi
