@@ -58,7 +58,7 @@ struct TraceArgs {
     double cert_tol32; // ... and of the single-precision estimate's bound
     unsigned long long *replay_count;   // Jones-vector variants: abandoned rays (local indices)
     uint32_t *replay_list;
-    // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, -} of
+    // Jones-vector variants: per-workgroup counter partials {bounces, bad_rays, eyebox_hits, interactions, ...} of
     // the trace kernel, summed into *stats by the epilogue -- no contended atomics on the stats
     unsigned long long *part;
     int n_trace_waves;                  // partial slots of the trace kernel (one per workgroup)

@@ -43,7 +43,7 @@ struct wgrt_scene {
         double2 *q_xy = nullptr;             // out-coupling queue: position, ray index
         uint32_t *q_i = nullptr;
         int64_t qcap = 0;
-        unsigned long long *part = nullptr;  // per-wave counter partials (4 words per slot)
+        unsigned long long *part = nullptr;  // per-wave counter partials (kPartWords words per slot)
         int64_t part_slots = 0;
         uint64_t *rng64 = nullptr;           // fused launches: per-ray {state, tag} granules
         uint32_t iter_epoch = 0;             // < 2^23 (iter_tag)
