@@ -30,6 +30,8 @@ dev = torch.device("cuda", 0)
 g, L, pts = build_inputs(w)
 sc = Scene.from_geometry(g, L, **json.loads(os.environ.get("AB_SCENE") or "{}"))
 lk = json.loads(os.environ.get("AB_LAUNCH") or "{}")
+_dbg = {k[4:]: lk.pop(k) for k in [k for k in lk if k.startswith("dbg_")]}   # +dbg_<field>=v: wgrt_debug_opts
+if _dbg: lk["debug"] = _dbg
 nshard = int(os.environ.get("AB_SHARD") or 1)   # trace rank 0's interleaved shard of nshard (strong scaling)
 shard = make_shard(nx, ny, len(lam), R, nshard, 0)
 rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(shard)
