@@ -1,4 +1,5 @@
-"""Build the in-tree HIP library ``libwgrt.so`` for gfx950 (hipcc, no JIT cache).
+"""Build the in-tree HIP library ``libwgrt.so`` for gfx950 (hipcc, no JIT cache) and the
+PyTorch-ROCm operator library ``_wgrt_torch.so`` over it (g++ against torch's headers).
 
 Called by ``__graft_entry__.build()``; safe to call repeatedly (rebuilds only when a
 source is newer than the library).
@@ -13,6 +14,8 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 CSRC = os.path.join(PKG, "csrc")
 REPO = os.path.dirname(PKG)
 LIB = os.path.join(PKG, "libwgrt.so")
+OPS_LIB = os.path.join(PKG, "_wgrt_torch.so")
+OPS_SOURCE = "wgrt_torch.cpp"
 SOURCES = ["wgrt_trace.hip", "wgrt_shadow.hip", "wgrt_scene_build.cpp"]
 HEADERS = ["wgrt_common.h", "wgrt_device.h", "wgrt_scene.h", "wgrt_scene_build.h"]
 ARCH = os.environ.get("WGRT_OFFLOAD_ARCH", "gfx950")
@@ -60,5 +63,32 @@ def build(force: bool = False, verbose: bool = False) -> str:
     return LIB
 
 
+def build_ops(force: bool = False, verbose: bool = False) -> str:
+    """``_wgrt_torch.so``: the ``torch.ops.wgrt`` operator library (csrc/wgrt_torch.cpp).  Host code
+    only (no kernels), so the host compiler builds it against the installed torch's headers and
+    libraries.  libwgrt.so is deliberately not linked: the operator calls the copy the Python layer
+    loaded (RTLD_GLOBAL, _lib.load); -z now makes a load without it fail at once."""
+    src = os.path.join(CSRC, OPS_SOURCE)
+    deps = [src, os.path.join(REPO, "include", "wgrt.h"), os.path.abspath(__file__)]
+    if not force and os.path.exists(OPS_LIB) and all(os.path.getmtime(d) <= os.path.getmtime(OPS_LIB) for d in deps):
+        return OPS_LIB
+    import torch
+    from torch.utils import cpp_extension
+    cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
+    abi = int(bool(torch._C._GLIBCXX_USE_CXX11_ABI))
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Werror", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           *[f"-I{p}" for p in cpp_extension.include_paths()], "-I", os.path.join(REPO, "include"), src,
+           *[f"-L{p}" for p in cpp_extension.library_paths()], "-lc10", "-ltorch", "-ltorch_cpu",
+           *[f"-Wl,-rpath,{p}" for p in cpp_extension.library_paths()], "-Wl,-z,now", "-o", OPS_LIB + ".tmp"]
+    if verbose:
+        print(" ".join(cmd))
+    out = subprocess.run(cmd, capture_output=True, text=True)
+    if out.returncode != 0:
+        raise RuntimeError("torch operator library build failed:\n" + out.stdout + out.stderr)
+    os.replace(OPS_LIB + ".tmp", OPS_LIB)
+    return OPS_LIB
+
+
 if __name__ == "__main__":
     print(build(force=True, verbose=True))
+    print(build_ops(force=True, verbose=True))

@@ -1,8 +1,10 @@
-"""ctypes binding of the in-tree HIP library ``libwgrt.so`` (C ABI: ``include/wgrt.h``).
+"""Bindings of the in-tree HIP library ``libwgrt.so`` (C ABI: ``include/wgrt.h``).
 
-This is the reference-side binding a Python caller uses; there is no CPU
-fallback: if the library is missing or cannot be loaded, every entry point
-raises ``WgrtError``.
+The scene, ray-setup and diagnostic entry points are bound with ctypes; the trace launch goes
+through the PyTorch-ROCm operator ``torch.ops.wgrt.trace`` (``_wgrt_torch.so``, built from
+csrc/wgrt_torch.cpp: ``ops()``), which forwards device tensors to ``wgrt_trace_opts`` of the same
+loaded library.  There is no CPU fallback: if either library is missing or cannot be loaded,
+every entry point raises ``WgrtError``.
 """
 from __future__ import annotations
 
@@ -14,6 +16,7 @@ import numpy as np
 PKG = os.path.dirname(os.path.abspath(__file__))
 # WGRT_LIB: load another build of the library (A/B measurements of build variants, tools/ab.py)
 LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
+OPS_PATH = os.path.join(PKG, "_wgrt_torch.so")   # the torch operator library (csrc/wgrt_torch.cpp)
 
 ABI_VERSION = 5
 # include/wgrt.h (the drop-in boundary) and include/wgrt_debug.h (test / profiling hooks)
@@ -115,7 +118,8 @@ def load(path: str = LIB_PATH):
         raise WgrtError(f"{path} not found: the HIP library is not built "
                         "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
     try:
-        L = ctypes.CDLL(path)
+        # RTLD_GLOBAL: the torch operator library (ops()) resolves the C ABI against this copy
+        L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     except OSError as e:
         raise WgrtError(f"cannot load {path}: {e}") from e
     st = ctypes.c_int
@@ -169,6 +173,28 @@ def load(path: str = LIB_PATH):
         raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} != expected {ABI_VERSION}")
     _lib = L
     return L
+
+
+_ops = None
+
+
+def ops():
+    """``torch.ops.wgrt``: the trace operator (``_wgrt_torch.so``), loaded after ``libwgrt.so``,
+    whose C ABI it calls (never builds implicitly)."""
+    global _ops
+    if _ops is not None:
+        return _ops
+    load()
+    if not os.path.exists(OPS_PATH):
+        raise WgrtError(f"{OPS_PATH} not found: the torch operator library is not built "
+                        "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
+    import torch
+    try:
+        torch.ops.load_library(OPS_PATH)
+    except OSError as e:
+        raise WgrtError(f"cannot load {OPS_PATH}: {e}") from e
+    _ops = torch.ops.wgrt
+    return _ops
 
 
 def check(status: int, what: str):

@@ -2,8 +2,9 @@
 
 ``trace_fullcolor`` is one launch of the bounce kernel (the reference's
 ``process_rays_kernel_pro_fullColor[blocks, 256](...)``, GRTF:833-1246) through the
-C ABI ``wgrt_trace_fullcolor_ex``; it validates every buffer and raises on misuse
-instead of corrupting memory.
+PyTorch-ROCm operator ``torch.ops.wgrt.trace`` (csrc/wgrt_torch.cpp), which forwards to the
+C ABI ``wgrt_trace_opts``; it validates every buffer and raises on misuse instead of
+corrupting memory.
 """
 from __future__ import annotations
 
@@ -13,7 +14,7 @@ import numpy as np
 import torch
 
 from . import _lib
-from ._lib import STATS_LEN, DebugOpts, LaunchOpts, Rays, Scene, TraceStats, WgrtError, check, load
+from ._lib import STATS_LEN, DebugOpts, Rays, Scene, TraceStats, WgrtError, check, load, ops
 
 RAY_COLUMNS = ("x", "y", "gap_x", "gap_y", "pol", "azi", "m", "n", "lmd_num", "te", "tm", "delta_phase")
 READ_COLUMNS = ("x", "y", "m", "n", "lmd_num", "te", "tm", "delta_phase")
@@ -164,9 +165,6 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
         if per_ray_bounces.dtype not in (torch.int32, torch.uint32):
             raise TypeError("per_ray_bounces must be uint32 / int32")
         _as_dev(per_ray_bounces, per_ray_bounces.dtype, "per_ray_bounces", device, x.numel())
-    r = Rays(**{k: ctypes.c_void_p(v.data_ptr()) for k, v in cols.items()})
-    for k in ("gap_x", "gap_y", "pol", "azi"):
-        setattr(r, k, ctypes.c_void_p(rays[k].data_ptr()) if k in rays else None)
     n_chunks = (N + CHUNK - 1) // CHUNK
     if chunk_order is not None:
         _as_dev(chunk_order, torch.int32, "chunk_order", device, n_chunks)
@@ -175,19 +173,14 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
             raise ValueError("gid_blocks needs gid_block_rays >= 1")
         _as_dev(gid_blocks, torch.int64, "gid_blocks", device, (N + gid_block_rays - 1) // gid_block_rays if N else None)
     dbg = _debug_opts(debug)
-    opts = LaunchOpts(1 if single else 0, int(variant), int(workgroups),
-                      ctypes.c_void_p(chunk_order.data_ptr()) if chunk_order is not None else None,
-                      n_chunks if chunk_order is not None else 0, int(num_iter),
-                      ctypes.c_void_p(gid_blocks.data_ptr()) if gid_blocks is not None else None,
-                      int(gid_block_rays) if gid_blocks is not None else 0,
-                      ctypes.pointer(dbg) if dbg is not None else None, float(grid_sqrt_k))
-    check(load().wgrt_trace_opts(
-        scene.handle, ctypes.byref(r), N, int(gid_offset), ctypes.c_void_p(rng_states.data_ptr()),
-        ctypes.c_void_p(matrix_EB.data_ptr()),
-        ctypes.c_void_p(stats.data_ptr()) if stats is not None else None,
-        ctypes.c_void_p(per_ray_bounces.data_ptr()) if per_ray_bounces is not None else None,
-        ctypes.c_void_p(_stream_handle(device, stream)), ctypes.byref(opts)),
-        "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
+    # the launch: torch.ops.wgrt.trace (csrc/wgrt_torch.cpp) -> wgrt_trace_opts on the caller's stream
+    status = ops().trace(scene.handle.value, cols["x"], cols["y"], cols["m"], cols["n"], cols.get("lmd_num"),
+                         cols["te"], cols["tm"], cols["delta_phase"], rng_states, matrix_EB, stats, per_ray_bounces,
+                         N, int(gid_offset), _stream_handle(device, stream), 1 if single else 0, int(variant),
+                         int(workgroups), chunk_order, int(num_iter), gid_blocks,
+                         int(gid_block_rays) if gid_blocks is not None else 0,
+                         ctypes.addressof(dbg) if dbg is not None else 0, float(grid_sqrt_k))
+    check(status, "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
 
 
 def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None):

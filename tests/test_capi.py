@@ -68,6 +68,45 @@ def test_struct_layouts_match_header(tmp_path):
             assert int(got[f"{c}.{f}"]) == getattr(py, f).offset, f"{c}.{f}"
 
 
+@pytest.fixture(scope="module")
+def wgrt_ops(lib):
+    torch = pytest.importorskip("torch")
+    if not os.path.exists(_lib.OPS_PATH):
+        import __graft_entry__
+        __graft_entry__.build()
+    return torch, _lib.ops()
+
+
+def test_torch_operator_schema(wgrt_ops):
+    """The PyTorch-ROCm operator the trace launches go through (csrc/wgrt_torch.cpp) is registered
+    with the reference kernel's in/out buffers marked as mutated."""
+    torch, ops = wgrt_ops
+    schema = str(ops.trace.default._schema)
+    assert schema.startswith("wgrt::trace(int scene, Tensor x, Tensor y, Tensor m, Tensor n, Tensor? lmd_num")
+    for arg in ("Tensor(a!) rng_states", "Tensor(b!) matrix_EB", "Tensor(c!)? stats", "Tensor(d!)? per_ray_bounces"):
+        assert arg in schema, arg
+    assert schema.endswith("-> int")
+
+
+def test_torch_operator_calls_only_the_c_abi(wgrt_ops):
+    """The operator library links no copy of the kernels: its only wgrt_ symbols are C-ABI entry
+    points, resolved against the libwgrt.so the Python layer loaded."""
+    out = subprocess.run(["nm", "-D", "--undefined-only", _lib.OPS_PATH], capture_output=True, text=True, check=True)
+    used = sorted({l.split()[-1] for l in out.stdout.splitlines() if l.split() and l.split()[-1].startswith("wgrt_")})
+    assert used == ["wgrt_scene_get_info", "wgrt_trace_opts"]
+    assert set(used) <= set(_lib.EXPORTED)
+    defined = subprocess.run(["nm", "-D", "--defined-only", _lib.OPS_PATH], capture_output=True, text=True, check=True)
+    assert "wgrt_" not in defined.stdout
+
+
+def test_torch_operator_rejects_null_scene(wgrt_ops):
+    torch, ops = wgrt_ops
+    t = torch.zeros(4)
+    with pytest.raises(RuntimeError, match="NULL scene"):
+        ops.trace(0, t, t, t, t, t, t, t, t, torch.zeros(4, dtype=torch.int32), torch.zeros(9600), None, None,
+                  4, 0, 0, 0, 0, 0, None, 1, None, 0, 0, 0.0)
+
+
 def test_abi_version_and_status_strings(lib):
     assert lib.wgrt_abi_version() == _lib.ABI_VERSION
     assert lib.wgrt_status_string(0) == b"ok"
