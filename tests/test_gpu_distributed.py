@@ -1,0 +1,129 @@
+"""The multi-GPU path with the HIP kernel in every rank (world size 2 and 3, all ranks on cuda:0, gloo).
+
+bench.py --gpus N's default (--scaling strong) on the product path: each rank lays out its
+interleaved FoV x wavelength shard on the device (``hip_shard_builder``, wgrt_rays_init), traces it
+through ``hip_tracer`` (torch.ops.wgrt.trace with the shard's ``gid_blocks``) inside
+``distributed.timed_run`` and the eyebox slabs are gathered to rank 0 (``EyeboxGather``; gloo moves
+device tensors through host copies, the one-GPU rehearsal of the RCCL gather).  Rank 0's grid and
+every rank's RNG states must equal the CPU oracle's single-process trace of the whole batch bit for
+bit, and the bounce SUM over ranks the oracle's total.  The replica mode (``--scaling weak``,
+sum-reduce) must equal the oracle's trace of the tiled batch.  RCCL itself needs one GPU per rank:
+its first run is the driver's 8-GPU bench.
+"""
+import os
+import socket
+
+import numpy as np
+import pytest
+
+torch = pytest.importorskip("torch")
+
+pytestmark = pytest.mark.gpu
+
+NX, NY, LAMBDAS, R, STEPS = 5, 4, [0, 1, 2], 256, 2
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _inputs():
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.couplers_coor import design_geometry
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import synthetic_luts
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import generate_points_in_polygon
+    geom = design_geometry(NX, NY)
+    luts = synthetic_luts(geom, seed=3, profile="deep")
+    pts = generate_points_in_polygon(geom.IC, R // 2, rng=np.random.default_rng(6))
+    return geom, luts, pts
+
+
+def _worker(rank, world, port, outdir, mode):
+    import torch.distributed as dist
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (EyeboxGather, hip_shard_builder,
+                                                                                hip_tracer, make_shard,
+                                                                                rank_blocks, replica_shard, timed_run)
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, check_stats, new_stats
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    dev = torch.device("cuda", 0)
+    torch.cuda.set_device(dev)
+    geom, luts, pts = _inputs()
+    scene = Scene.from_geometry(geom, luts)
+    nb = NX * NY * len(LAMBDAS)
+    if mode == "strong":
+        shard = make_shard(NX, NY, len(LAMBDAS), R, world, rank)
+        collect = EyeboxGather([rank_blocks(nb, world, r, "interleaved", len(LAMBDAS)) for r in range(world)],
+                               NX, NY, LAMBDAS, len(LAMBDAS), device=dev)
+    else:
+        shard = replica_shard(NX, NY, len(LAMBDAS), R, world, rank)
+        collect = None   # sum-reduce
+    rays, rng = hip_shard_builder(pts, NX, NY, LAMBDAS, R, dev)(shard)
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    stats = new_stats(dev)
+    el, tot, loc = timed_run(hip_tracer(scene, 0, stats), rays, rng, eb, shard.gid, STEPS, 1, stats,
+                             sync=torch.cuda.synchronize, collect=collect)
+    check_stats(stats)
+    np.save(os.path.join(outdir, f"rng{rank}.npy"), rng.cpu().numpy())
+    np.save(os.path.join(outdir, f"blocks{rank}.npy"), shard.blocks)
+    np.save(os.path.join(outdir, f"res{rank}.npy"), np.array([el, tot, loc], dtype=np.float64))
+    if rank == 0:
+        np.save(os.path.join(outdir, "eb.npy"), eb.cpu().numpy())
+    scene.close()
+    dist.destroy_process_group()
+
+
+def _oracle(copies=1):
+    """The oracle's STEPS chained traces of the batch (``copies`` tiled replicas, global ids
+    continuing across them): final RNG states, grid, bounces."""
+    from oracle import OracleScene
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import shard_rays_host
+    geom, luts, pts = _inputs()
+    nb = NX * NY * len(LAMBDAS)
+    rays, rng = shard_rays_host(pts, NX, NY, LAMBDAS, R, np.arange(nb))
+    if copies > 1:
+        from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import rng_seeds
+        rays = {k: np.concatenate([v] * copies) for k, v in rays.items()}
+        rng = rng_seeds(copies * nb * R, 0)
+    sc = OracleScene.from_geometry(geom, luts)
+    eb = np.zeros(sc.eb_shape(), np.float32)
+    tot = sum(sc.trace(rays, rng, eb, threads=8)[0] for _ in range(STEPS))
+    return rng, eb, tot
+
+
+def _run(tmp_path, world, mode):
+    import torch.multiprocessing as mp
+    if not torch.cuda.is_available():
+        pytest.skip("no HIP device")
+    mp.start_processes(_worker, args=(world, _free_port(), str(tmp_path), mode), nprocs=world, join=True,
+                       start_method="spawn")
+    return [np.load(tmp_path / f"res{r}.npy") for r in range(world)]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_strong_shards_on_device_equal_oracle(tmp_path, world):
+    res = _run(tmp_path, world, "strong")
+    rng, eb, tot = _oracle()
+    assert all(int(r[1]) == tot for r in res)               # SUM of the ranks' device counters
+    assert all(r[2] > 0 for r in res)
+    np.testing.assert_array_equal(np.load(tmp_path / "eb.npy"), eb)
+    assert eb.sum() > 0
+    for r in range(world):
+        blocks = np.load(tmp_path / f"blocks{r}.npy")
+        got = np.load(tmp_path / f"rng{r}.npy").view(np.uint32)
+        np.testing.assert_array_equal(got, rng.reshape(-1, R)[blocks].reshape(-1), err_msg=f"rank {r}")
+
+
+def test_replicas_on_device_equal_oracle(tmp_path):
+    world = 2
+    res = _run(tmp_path, world, "weak")
+    rng, eb, tot = _oracle(copies=world)
+    assert all(int(r[1]) == tot for r in res)
+    np.testing.assert_array_equal(np.load(tmp_path / "eb.npy"), eb)
+    n = len(rng) // world
+    for r in range(world):
+        np.testing.assert_array_equal(np.load(tmp_path / f"rng{r}.npy").view(np.uint32), rng[r * n:(r + 1) * n],
+                                      err_msg=f"replica {r}")
