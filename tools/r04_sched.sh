@@ -1,6 +1,8 @@
 #!/bin/bash
 # Round-4 A/B of the AMDGPU machine scheduler strategy (exp_libs built by tools/ab_build.py with
 # -mllvm -amdgpu-sched-strategy=...) against the tree's library, on C3, C2 and C4.
+# (The exp_libs builds: python tools/ab_build.py silp=-mllvm,-amdgpu-sched-strategy=max-ilp
+#  smem=-mllvm,-amdgpu-sched-strategy=max-memory-clause sitilp=-mllvm,-amdgpu-sched-strategy=iterative-ilp)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for c in ${CONFIGS:-C3 C2 C4}; do

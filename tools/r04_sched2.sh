@@ -1,5 +1,6 @@
 #!/bin/bash
 # Round-4: the scheduler-strategy builds on the latency-bound launches (C2, C3 shards of 8 / 4 / 2 ranks).
+# (exp_libs as in tools/r04_sched.sh)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 mkdir -p gpurun_out
 for spec in ${CASES:-C2:1 C3:8 C3:4 C3:2}; do
