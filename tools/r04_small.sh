@@ -2,8 +2,8 @@
 # Round-4 small-batch A/B: GPU parity of the tree's library (TESTS), then tools/ab.py over the small-batch
 # selection (never / auto / always) on C2, the C3 shards of 8, 4 and 2 ranks, and C3.  Each step under its
 # own time limit; stops at the first failure.
-# (Ran on the small-batch build of commit 5b6968b's parent tree; that instantiation and its
-# wgrt_debug_opts.small_batch field were removed after this A/B, so the script no longer runs as is.)
+# (Ran on a build that added trace_jones_small_kernel and wgrt_debug_opts.small_batch; both were removed
+# after this A/B without being committed, so the script no longer runs as is.)
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 OUT=$(pwd)/gpurun_out
 TAG=${TAG:-r04sb}
