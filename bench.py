@@ -99,8 +99,8 @@ def config_for(name: str, world: int):
 
 
 def lib_sha16() -> str:
-    from gpu_ray_tracing_for_waveguide_based_ar_display_amd._lib import LIB_PATH
-    with open(LIB_PATH, "rb") as f:
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd._lib import loaded_path
+    with open(loaded_path(), "rb") as f:
         return hashlib.sha256(f.read()).hexdigest()[:16]
 
 

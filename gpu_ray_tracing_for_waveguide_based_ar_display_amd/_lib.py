@@ -14,8 +14,7 @@ import os
 import numpy as np
 
 PKG = os.path.dirname(os.path.abspath(__file__))
-# WGRT_LIB: load another build of the library (A/B measurements of build variants, tools/ab.py)
-LIB_PATH = os.environ.get("WGRT_LIB") or os.path.join(PKG, "libwgrt.so")
+LIB_PATH = os.path.join(PKG, "libwgrt.so")   # the in-tree build, the only one the product binds
 OPS_PATH = os.path.join(PKG, "_wgrt_torch.so")   # the torch operator library (csrc/wgrt_torch.cpp)
 
 ABI_VERSION = 5
@@ -107,13 +106,31 @@ class SceneInfo(ctypes.Structure):
 
 
 _lib = None
+_lib_path = LIB_PATH
+_accept_abi = (ABI_VERSION,)
 
 
-def load(path: str = LIB_PATH):
+def use_library(path: str, accept_abi=(ABI_VERSION,)) -> None:
+    """Tools only (tools/with_lib.py: A/B timing of build variants, tools/ab.py): bind another build of
+    the library, optionally of an earlier ABI whose structs are prefixes of this one's, instead of the
+    in-tree one.  Must run before anything loads the library; the product never calls it."""
+    global _lib_path, _accept_abi
+    if _lib is not None:
+        raise WgrtError(f"libwgrt is already loaded from {_lib_path}")
+    _lib_path, _accept_abi = os.path.abspath(path), tuple(accept_abi)
+
+
+def loaded_path() -> str:
+    """The library file load() binds (the in-tree build unless a tool chose another)."""
+    return _lib_path
+
+
+def load():
     """Load libwgrt.so (never builds implicitly: build with ``__graft_entry__.build()``)."""
     global _lib
     if _lib is not None:
         return _lib
+    path = _lib_path
     if not os.path.exists(path):
         raise WgrtError(f"{path} not found: the HIP library is not built "
                         "(run `python -c 'import __graft_entry__ as g; g.build()'`)")
@@ -167,9 +184,7 @@ def load(path: str = LIB_PATH):
     L.wgrt_last_error.restype = ctypes.c_char_p
     L.wgrt_last_error.argtypes = []
     L.wgrt_abi_version.restype = ctypes.c_int
-    # WGRT_ABI_ANY=1: accept an ABI-4 build too (A/B timing of an earlier build through this binding: its
-    # structs are prefixes of ABI 5's)
-    if L.wgrt_abi_version() != ABI_VERSION and not (os.environ.get("WGRT_ABI_ANY") and L.wgrt_abi_version() == 4):
+    if L.wgrt_abi_version() not in _accept_abi:
         raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} != expected {ABI_VERSION}")
     _lib = L
     return L

@@ -82,28 +82,69 @@ struct TraceArgs {
 
 constexpr int kPartWords = 8;   // counter partial slot of a trace workgroup (64-bit words)
 
-// A TraceArgs field of the kernel's first argument, re-read from the kernarg segment where it is
-// used (a volatile scalar load, a scalar-cache hit) instead of being held in an SGPR for the
-// whole kernel: the Jones loop keeps only its per-pass operands in SGPRs; the ray columns and
-// the rare-path pointers (refill, retire, replay, out-coupling) are fetched when those run.
-// Valid only in kernels whose first parameter is the TraceArgs.
-template <class T>
-__device__ __forceinline__ T karg(size_t off) {
-    typedef volatile const T __attribute__((address_space(4))) *VP;
-    const char __attribute__((address_space(4))) *base =
-        (const char __attribute__((address_space(4))) *)__builtin_amdgcn_kernarg_segment_ptr();
-    return *(VP)(base + off);
+// TraceArgs fields re-read from the kernarg segment where they are used (a volatile scalar load,
+// a scalar-cache hit) instead of being held in SGPRs for the whole kernel: the Jones loop keeps
+// only its per-pass operands in SGPRs; the ray columns and the rare-path pointers (refill,
+// retire, replay, out-coupling) are fetched when those run.
+//
+// KArgs is the handle those reads go through: the base of the kernarg segment as the KERNEL BODY
+// saw it.  Only kernel_kargs<Kernel>() makes one, and it refuses to compile unless Kernel's first
+// parameter is a TraceArgs (which then lies at offset 0 of the segment).  A function that reads a
+// field takes the handle as a parameter, so it reads the right segment whether or not the
+// compiler inlines it; __builtin_amdgcn_kernarg_segment_ptr() evaluated inside a called function
+// instead reads whatever the caller's registers hold (round 4's out-of-line EDGE build faulted
+// with hipErrorIllegalAddress that way).
+typedef const char __attribute__((address_space(4))) KSeg;
+
+template <class F>
+struct first_param;
+template <class A0, class... R>
+struct first_param<void(A0, R...)> {
+    using type = A0;
+};
+template <class X, class Y>
+struct same_type {
+    static constexpr bool value = false;
+};
+template <class X>
+struct same_type<X, X> {
+    static constexpr bool value = true;
+};
+
+class KArgs {
+    KSeg *base_;
+    __device__ explicit KArgs(KSeg *b) : base_(b) {}
+    template <class Kernel>
+    friend __device__ KArgs kernel_kargs();
+
+public:
+    template <class T>
+    __device__ __forceinline__ T get(size_t off) const {
+        return *(volatile const T __attribute__((address_space(4))) *)(base_ + off);
+    }
+};
+
+// Call in the body of the __global__ function Kernel itself: kernel_kargs<decltype(my_kernel<...>)>().
+template <class Kernel>
+__device__ __forceinline__ KArgs kernel_kargs() {
+    static_assert(same_type<typename first_param<Kernel>::type, TraceArgs>::value,
+                  "KArgs reads TraceArgs fields at their offsets in the kernarg segment: the kernel's first "
+                  "parameter must be the TraceArgs");
+    return KArgs((KSeg *)__builtin_amdgcn_kernarg_segment_ptr());
 }
-#define KA(f) karg<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
+
+// A TraceArgs field through the handle K in scope.
+#define KA(f) K.template get<decltype(TraceArgs::f)>(offsetof(TraceArgs, f))
 // the same for the locator's exact-test arrays (TraceArgs::loc holds them for every variant)
-#define KLOC(f) karg<decltype(Locator::f)>(offsetof(TraceArgs, loc) + offsetof(Locator, f))
+#define KLOCP(Kp, f) (Kp)->template get<decltype(Locator::f)>(offsetof(TraceArgs, loc) + offsetof(Locator, f))
+#define KLOC(f) KLOCP(&K, f)
 
 // Global id of local ray i (wgrt_launch_opts.gid_blocks): only the zero-state RNG fix-up reads it.
 __device__ __forceinline__ int64_t ray_gid(const TraceArgs &A, int64_t i) {
     return A.gid_blocks ? A.gid_blocks[i / A.gid_block_rays] + i % A.gid_block_rays : A.gid_offset + i;
 }
-// The same from the kernarg segment (kernels whose first parameter is the TraceArgs).
-__device__ __forceinline__ int64_t ray_gid_ka(int64_t i) {
+// The same from the kernarg segment.
+__device__ __forceinline__ int64_t ray_gid_ka(const KArgs &K, int64_t i) {
     const int64_t *gb = KA(gid_blocks);
     if (gb) {
         const int64_t r = KA(gid_block_rays);
@@ -179,15 +220,23 @@ __device__ __forceinline__ typename Loc::Word locate_w(const Loc &L, double x, d
     return L.cells[(int)fy * L.ncx + (int)fx];
 }
 
-template <bool KARG = false, class Loc>
-__device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y) {
+// The exact test of an EDGE class.  Kp: the launch's kernarg handle -- the locator's array pointers
+// are then read from the kernarg segment (not held in SGPRs across the Jones loop); NULL: from L.
+template <class Loc>
+#ifdef WGRT_EDGE_NOINLINE
+__device__ __attribute__((noinline))   // A/B and contract check: the exact tests as a real call
+#else
+__device__ __forceinline__
+#endif
+bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y, const KArgs *Kp = nullptr) {
     const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
     if (cls != 2u) return cls == 1u;
     const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
     const int r = k * L.ncy + cy;
+    const bool KARG = Kp != nullptr;
     // one 128-B record: the (at most kBandSegs) edges of polygon k meeting this cell row,
     // evaluated with the reference predicate's operations (GRTF:36-71); NaN slots are inert
-    const double *const bands = KARG ? KLOC(bands) : L.bands;
+    const double *const bands = KARG ? KLOCP(Kp, bands) : L.bands;
     const double4 *rec = (const double4 *)(bands + (size_t)r * 4 * kBandSegs);
     const double4 s0 = rec[0], s1 = rec[1], s2 = rec[2], s3 = rec[3];
     if (s0.x != INFINITY) {
@@ -201,29 +250,12 @@ __device__ __forceinline__ bool in_poly_w(const Loc &L, typename Loc::Word w, in
         }
         return inside;
     }
-    const int32_t *const po = KARG ? KLOC(poly_off) : L.poly_off;
-    const int32_t *const ro = KARG ? KLOC(row_off) : L.row_off;
+    const int32_t *const po = KARG ? KLOCP(Kp, poly_off) : L.poly_off;
+    const int32_t *const ro = KARG ? KLOCP(Kp, row_off) : L.row_off;
     const int a = po[k], nv = po[k + 1] - a;
     const int e0 = ro[r], e1 = ro[r + 1];
-    return inside_or_on_edge_subset(x, y, (KARG ? KLOC(verts) : L.verts) + 2 * a, nv,
-                                    (KARG ? KLOC(row_edges) : L.row_edges) + e0, e1 - e0);
-}
-
-template <bool KARG = false, class Loc>
-__device__ __forceinline__ int first_slice_w(const Loc &L, typename Loc::Word w, int first, int count, double x,
-                                             double y) {
-    uint64_t f = (uint64_t)w >> (2 * first);
-    if (count < 32) f &= (1ull << (2 * count)) - 1ull;
-    const uint64_t in = f & 0x5555555555555555ull;
-    uint64_t cand = in | ((f >> 1) & 0x5555555555555555ull);
-    while (cand != 0ull) {
-        const int p = __builtin_ctzll(cand);
-        const int sl = p >> 1;
-        if ((in >> p) & 1ull) return sl;
-        if (in_poly_w<KARG>(L, w, first + sl, x, y)) return sl;
-        cand &= cand - 1ull;
-    }
-    return -1;
+    return inside_or_on_edge_subset(x, y, (KARG ? KLOCP(Kp, verts) : L.verts) + 2 * a, nv,
+                                    (KARG ? KLOCP(Kp, row_edges) : L.row_edges) + e0, e1 - e0);
 }
 
 // E_field_cal (GRTF:132-152).  rec = (p, q, r, s) complex in the reference call's argument
@@ -601,6 +633,7 @@ struct JLane {
     uint32_t tix;            // this ray's (lambda, m, n) tile index (its Jones tile: jtiles + tix * jtile_d)
     uint32_t i;              // local ray index (variants 7 / 9: < 2^32)
     uint32_t bounces;
+    uint32_t inter;          // interactions of this trace after the in-coupling event (wgrt_trace_stats.interactions)
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
     uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
@@ -640,7 +673,7 @@ __device__ __forceinline__ void glds4(const void *g, LdsU32 *dst) {
 }
 
 // Issued by the lanes j < n of a wave (exec-masked): column c of ray base + j -> S[c * 64 + j].
-__device__ __forceinline__ void stage_chunk(const TraceArgs &A, LdsU32 *S, int64_t ray) {
+__device__ __forceinline__ void stage_chunk(const KArgs &K, LdsU32 *S, int64_t ray) {
     glds4(KA(x) + ray, S + 0 * 64);
     glds4(KA(y) + ray, S + 1 * 64);
     glds4(KA(m) + ray, S + 2 * 64);
@@ -655,7 +688,7 @@ __device__ __forceinline__ void stage_chunk(const TraceArgs &A, LdsU32 *S, int64
 
 // Slot j of a staged chunk (its loads have landed) -> the ray's start state, in place: lane j
 // of the wave that dequeued the chunk, for every ray of it at once.
-__device__ __forceinline__ void prep_staged(const TraceArgs &A, LdsU32 *S, int j) {
+__device__ __forceinline__ void prep_staged(const TraceArgs &A, const KArgs &K, LdsU32 *S, int j) {
     const int m = (int)__uint_as_float(S[2 * 64 + j]), n = (int)__uint_as_float(S[3 * 64 + j]);
     const int l = KA(l) ? (int)__uint_as_float(S[4 * 64 + j]) : 0;
     const float ftm = __uint_as_float(S[6 * 64 + j]), d = __uint_as_float(S[7 * 64 + j]);
@@ -695,6 +728,7 @@ __device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t
     L.r.hi = 0.0;
     L.r.region = 0;
     L.bounces = 1;
+    L.inter = 0;
     // L.pf is not set: the first pass runs the in-coupling interaction, which loads it (and a
     // write here would wait for the cell loads other lanes' miss hops have in flight)
     return tix != kBadTix;
@@ -855,8 +889,8 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // double-precision matrix (loaded after the decision), so the carried Jones vector and ener
 // are the same values the all-double evaluation gives.
 template <bool SINGLE, class Loc>
-__device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLane &L, int blk, int kind,
-                                        bool entry) {
+__device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
+                                        int kind, bool entry) {
     JRay &r = L.r;
     const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
@@ -874,7 +908,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     const double2 mva = *(const double2 *)(T + kJGap + ga);
     const double2 mvb = *(const double2 *)(T + kJGap + gb);
     const double denom = entry ? cg.x : r.cos_t;
-    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka((int64_t)L.i); });
+    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
@@ -924,7 +958,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
     r.hr = hop.x;
     r.hi = hop.y;
     if (kind == 0) {
-        const bool in_ic = in_poly_w<true>(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y);
+        const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y, &K);
         if (ba) return in_ic ? 0 : 2;
         return in_ic ? 1 : kDie;
     }
@@ -936,12 +970,12 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, JLan
 // first IN one, eff_reg2's in R3 -- replaced by the exact predicate's verdict (IN 1 / OUT 0) through
 // the 128-B band records (in_poly_w).  Rare: 0.34 % of C3 lane-passes meet an EDGE cell.
 template <class Loc>
-__device__ __forceinline__ typename Loc::Word resolve_edges(const Loc &loc, typename Loc::Word w, int region, int first,
-                                                            int count, double x, double y) {
+__device__ __forceinline__ typename Loc::Word resolve_edges(const KArgs &K, const Loc &loc, typename Loc::Word w,
+                                                            int region, int first, int count, double x, double y) {
     using W = typename Loc::Word;
     auto fix = [&](int k) {
         if (((w >> (2 * k)) & 3u) == 2u) {
-            const bool in = in_poly_w<true>(loc, w, k, x, y);
+            const bool in = in_poly_w(loc, w, k, x, y, &K);
             w = (W)((w & ~((W)3 << (2 * k))) | ((W)(in ? 1u : 0u) << (2 * k)));
         }
     };
@@ -969,7 +1003,7 @@ __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); 
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
 template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane &L, int &kind) {
+__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
@@ -988,7 +1022,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, JLane
     const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
     const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
     if (e1edge | sedge | e2edge) {
-        c = resolve_edges(loc, c, region, first, count, r.x, r.y);
+        c = resolve_edges(K, loc, c, region, first, count, r.x, r.y);
         f = (c >> (2 * first)) & gmask;
         in = f & kLow;
         cand = in | ((f >> 1) & kLow);

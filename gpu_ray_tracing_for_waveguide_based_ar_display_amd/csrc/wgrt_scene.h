@@ -58,6 +58,35 @@ namespace wgrt {
 // Record the detail of a failing entry point for wgrt_last_error() and return its status.
 wgrt_status fail(wgrt_status s, const std::string &msg);
 
+// The C ABI's device discipline: an entry point that works on a scene (or allocates, or launches on
+// a stream) makes the scene's device current for its own scope and gives the caller's current
+// device back when it returns, so a host that drives several GPUs from one thread keeps whatever
+// device it had selected.  hipSetDevice only when the device differs (a thread-local switch).
+class DeviceScope {
+    int prev_ = -1;
+    hipError_t err_ = hipSuccess;
+
+public:
+    explicit DeviceScope(int device) {
+        err_ = hipGetDevice(&prev_);
+        if (err_ != hipSuccess) prev_ = -1;
+        else if (prev_ != device) err_ = hipSetDevice(device);
+    }
+    ~DeviceScope() {
+        int cur = -1;
+        if (prev_ >= 0 && hipGetDevice(&cur) == hipSuccess && cur != prev_) (void)hipSetDevice(prev_);
+    }
+    DeviceScope(const DeviceScope &) = delete;
+    DeviceScope &operator=(const DeviceScope &) = delete;
+    hipError_t error() const { return err_; }
+};
+
+// The device a stream belongs to (the current device for the null stream).
+inline hipError_t stream_device(void *stream, int *device) {
+    if (!stream) return hipGetDevice(device);
+    return hipStreamGetDevice((hipStream_t)stream, device);
+}
+
 inline Locator make_locator(const wgrt_scene *s) {
     Locator L;
     L.cells = s->d_cells;

@@ -363,6 +363,9 @@ extern "C" wgrt_status wgrt_debug_shadow(const wgrt_scene *s, const wgrt_rays *r
     A.cert_tol = kCertTol;   // the bounds the product lane uses by default
     A.cert_tol32 = std::max(kCertTol32, A.cert_tol);
     S.out = stats;
+    DeviceScope dev_scope(s->device);   // launched on the scene's device; the caller's is restored
+    if (dev_scope.error() != hipSuccess)
+        return fail(WGRT_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(dev_scope.error()));
     const int64_t blocks = std::min<int64_t>((n_rays + 255) / 256, 16384);
     hipLaunchKernelGGL(shadow_kernel<Locator>, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, S, A.loc);
     const hipError_t e = hipGetLastError();

@@ -16,6 +16,7 @@
 #include <torch/library.h>
 
 #include <ATen/core/Tensor.h>
+#include <c10/core/DeviceGuard.h>
 
 #include <cstdint>
 #include <optional>
@@ -64,6 +65,9 @@ int64_t trace(int64_t scene, const Tensor &x, const Tensor &y, const Tensor &m, 
     const wgrt_status st = wgrt_scene_get_info(s, &info);
     if (st != WGRT_OK) return st;
     const Ctx c{c10::Device(c10::DeviceType::CUDA, static_cast<c10::DeviceIndex>(info.device)), x.numel()};
+    // the scene's device is current for the call (the library selects it too, include/wgrt.h) and the
+    // caller's comes back on return
+    const c10::DeviceGuard guard(c.dev);
     TORCH_CHECK(n_rays >= 0 && n_rays <= c.rays, "wgrt.trace: n_rays=", n_rays, " out of range for ", c.rays, " rays");
     TORCH_CHECK(kernel == 0 || kernel == 1, "wgrt.trace: kernel must be 0 (full colour) or 1 (single wavelength)");
 

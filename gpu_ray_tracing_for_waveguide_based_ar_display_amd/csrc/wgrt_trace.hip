@@ -57,6 +57,11 @@ namespace {
 constexpr double kDefaultCellMm = WGRT_CELL_MM;
 
 
+#define DEVICE_SCOPE(name, dev)                                                                      \
+    DeviceScope name(dev);                                                                          \
+    if (name.error() != hipSuccess)                                                                 \
+        return fail(WGRT_ERR_HIP, std::string("hipSetDevice: ") + hipGetErrorString(name.error()))
+
 #define HIP_TRY(expr)                                                                       \
     do {                                                                                    \
         hipError_t e_ = (expr);                                                             \
@@ -224,7 +229,8 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
 // TL: the debug wave timeline (wgrt_debug_opts.timeline); the product instantiations have TL = false
 // and contain none of its code.
 template <bool FUSED, bool SINGLE, bool TL, class Loc>
-__device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, unsigned long long *heads, int chunk) {
+__device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, const Loc &loc, unsigned long long *heads,
+                                          int chunk) {
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
@@ -320,16 +326,31 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         kind = 0;
         entry = true;
     };
+    // a trace's counters are added when it ends: an abandoned trace (kUncertain) adds nothing, and its
+    // replay (epilogue_kernel, trace_one) counts the whole trace once
     auto retire = [&]() {
         tot_b += L.bounces;
+        tot_int += L.inter;
         if (tot_b >= 0x80000000u) {
             wgrt_trace_stats *const st = KA(stats);
             if (st) atomicAdd((unsigned long long *)&st->bounces, (unsigned long long)tot_b);
             tot_b = 0;
         }
         if (FUSED && (int64_t)L.k + 1 < n_iter) {
-            __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false),
-                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            const uint64_t hand = ((uint64_t)L.r.s << 32) | iter_tag(A.iter_epoch, L.k + 1, false);
+            if (L.k > 0) {
+                // the granule still holds what this trace started from, unless the waiter for the next
+                // trace has given up and marked the ray abandoned meanwhile: the mark then stays (a
+                // compare-and-swap whose result is not used: no return, no wait), so the ray's later
+                // traces skip it instead of each waiting out the bound again
+                uint64_t was = ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, false);
+                __hip_atomic_compare_exchange_strong(KA(rng64) + L.i, &was, hand, __ATOMIC_RELAXED,
+                                                     __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            } else {
+                // trace 0 read no granule (its start state is rng_states): a give-up that raced this
+                // store costs the ray's next waiter one more bound before it gives up too
+                __hip_atomic_store(KA(rng64) + L.i, hand, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            }
         } else {
             KA(rng)[L.i] = L.r.s;
             uint32_t *const pr = KA(per_ray);
@@ -348,8 +369,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         }
         bool out = false;
         if (active && blk >= 0) {
-            tot_int += entry ? 0u : 1u;
-            const int next = interact<SINGLE>(A, loc, L, blk, kind, entry);
+            L.inter += entry ? 0u : 1u;
+            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
                 retire();
@@ -395,7 +416,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
 
     for (;;) {
         if (active) {
-            blk = advance(A, loc, L, kind);
+            blk = advance(A, K, loc, L, kind);
             entry = false;
             if (blk == kDie) retire();
         }
@@ -416,12 +437,17 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 waiting = false;   // abandoned in an earlier iteration: the replay kernel finishes it
             } else if ((++wait_passes > A.handoff_min_passes) &
                        (__builtin_amdgcn_s_memrealtime() - wait_t0 > A.handoff_wait_ticks)) {
-                waiting = false;   // hand-off never arrived: give the trace up, visibly
-                ++tot_giveup;
-                // and mark the ray abandoned from this trace on, so that its later traces skip it instead of
-                // each waiting out the bound again (the call's results are invalid; the Python layer raises)
-                __hip_atomic_store(KA(rng64) + L.i, (uint64_t)iter_tag(A.iter_epoch, L.k, true), __ATOMIC_RELAXED,
-                                   __HIP_MEMORY_SCOPE_AGENT);
+                // hand-off never arrived: give the trace up, visibly, and mark the ray abandoned from this
+                // trace on, so that its later traces skip it instead of each waiting out the bound again (the
+                // call's results are invalid; the Python layer raises).  Only if the granule still holds the
+                // value just polled: a hand-off that arrived since is taken by the next pass's poll instead
+                uint64_t seen = w;
+                if (__hip_atomic_compare_exchange_strong(KA(rng64) + L.i, &seen,
+                                                         (uint64_t)iter_tag(A.iter_epoch, L.k, true), __ATOMIC_RELAXED,
+                                                         __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT)) {
+                    waiting = false;
+                    ++tot_giveup;
+                }
             }
         }
         uint64_t need = __ballot(!active && !waiting);
@@ -471,7 +497,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
                 sbase_prev = sbase;
                 sbase = (uint32_t)cur;
                 ++staged;
-                if (lane < (int)(end - cur)) stage_chunk(A, sbufs + sb * (kStageCols * 64), cur + lane);
+                if (lane < (int)(end - cur)) stage_chunk(K, sbufs + sb * (kStageCols * 64), cur + lane);
             }
             const int want = __popcll(need);
             const int64_t avail = end - cur;
@@ -493,7 +519,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
             // lane j prepares slot j of the new chunk; the LDS stores precede the refilled lanes'
             // reads of other lanes' slots in the wave's (in-order) LDS queue
-            if (lane < (int)(end - (int64_t)sbase)) prep_staged(A, sbufs + sb * (kStageCols * 64), lane);
+            if (lane < (int)(end - (int64_t)sbase)) prep_staged(A, K, sbufs + sb * (kStageCols * 64), lane);
             asm volatile("" ::: "memory");
         }
         if (taken) {
@@ -515,7 +541,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const Loc &loc, u
         // The first pass continues the one the main loop broke off (advance and refill done).
         for (bool first = true;; first = false) {
             if (!first && active) {
-                blk = advance(A, loc, L, kind);
+                blk = advance(A, K, loc, L, kind);
                 entry = false;
                 if (blk == kDie) retire();
             }
@@ -584,7 +610,8 @@ constexpr int jones_waves() {
 template <class CellT, bool FUSED, bool SINGLE>
 __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    jones_body<FUSED, SINGLE, false>(A, loc, counter, chunk);
+    jones_body<FUSED, SINGLE, false>(A, kernel_kargs<decltype(trace_jones_kernel<CellT, FUSED, SINGLE>)>(), loc, counter,
+                                     chunk);
 }
 
 // The same loop with the debug wave timeline (wgrt_debug_opts.timeline; tools/timeline.py): a
@@ -592,7 +619,8 @@ __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void tr
 template <class CellT, bool FUSED, bool SINGLE>
 __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_tl_kernel(
     TraceArgs A, LocatorT<CellT> loc, unsigned long long *counter, int chunk) {
-    jones_body<FUSED, SINGLE, true>(A, loc, counter, chunk);
+    jones_body<FUSED, SINGLE, true>(A, kernel_kargs<decltype(trace_jones_tl_kernel<CellT, FUSED, SINGLE>)>(), loc,
+                                    counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -813,7 +841,7 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
     } catch (const std::exception &e) {
         return fail(WGRT_ERR_INVALID_ARGUMENT, e.what());
     }
-    HIP_TRY(hipSetDevice(device));
+    DEVICE_SCOPE(dev_scope, device);   // the caller's current device is restored on return
     auto *s = new wgrt_scene();
     s->device = device;
     s->nx = d.nx;
@@ -953,7 +981,7 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
 
 wgrt_status wgrt_scene_destroy(wgrt_scene *s) {
     if (!s) return WGRT_OK;
-    (void)hipSetDevice(s->device);
+    DeviceScope dev_scope(s->device);
     (void)hipFree(s->d_tiles);
     (void)hipFree(s->d_jtiles);
     (void)hipFree(s->d_cells);
@@ -1124,6 +1152,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
                          void *stream, LaunchCfg c) {
     if (!s || !rays) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene / rays");
     if (n_rays < 0 || gid_offset < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative n_rays / gid_offset");
+    // launch scratch is allocated and the kernels launched on the scene's device
+    DEVICE_SCOPE(dev_scope, s->device);
     const bool single = c.single;
     int variant = c.variant;
     int num_iter = c.num_iter;
@@ -1217,7 +1247,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     // a workgroup's 4 waves need 4 work items to all have work (debug chunk_rays: smaller items)
     const int64_t item = (dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk;
     const int64_t useful = (n_rays + 4 * item - 1) / (4 * item);
-    if (c.workgroups <= 0 && !timeline && num_iter <= 1 && c.grid_k >= 0.0) {
+    if (c.workgroups <= 0 && num_iter <= 1 && c.grid_k >= 0.0) {
         // a single trace ends with the drain of its longest ray chains, and chains run faster
         // on a less crowded chip, while the bulk before it wants every resident wave: the grid
         // that balances bulk throughput (work / W) against drain crowding (~ W) grows as
@@ -1319,6 +1349,7 @@ wgrt_status wgrt_scene_reserve(const wgrt_scene *s, int64_t n_rays, int num_iter
     if (!s) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL scene");
     if (n_rays < 0 || num_iter < 0 || num_iter > 255) return fail(WGRT_ERR_INVALID_ARGUMENT, "bad n_rays / num_iter");
     if (n_rays == 0) return WGRT_OK;
+    DEVICE_SCOPE(dev_scope, s->device);
     int64_t grid = 0;
     for (int c = 0; c < 2; ++c)
         for (int f = 0; f < 2; ++f)
@@ -1378,6 +1409,7 @@ wgrt_status wgrt_scene_classify(const wgrt_scene *s, const double *xy, int64_t n
                                 void *stream) {
     if (!s || (n > 0 && (!xy || !out_mask))) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n <= 0) return WGRT_OK;
+    DEVICE_SCOPE(dev_scope, s->device);
     const int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(classify_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream,
                        make_locator(s), s->npoly, xy, n, out_mask);
@@ -1409,6 +1441,10 @@ wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t n
     A.nl = n_lambdas;
     for (int k = 0; k < n_lambdas; ++k) A.lambdas[k] = (float)lambdas[k];
     if (A.n == 0) return WGRT_OK;
+    // no scene: the kernel runs on the stream's device
+    int sdev = 0;
+    HIP_TRY(stream_device(stream, &sdev));
+    DEVICE_SCOPE(dev_scope, sdev);
     const int64_t blocks = std::min<int64_t>((A.n + 255) / 256, 65536);
     hipLaunchKernelGGL(rays_init_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A);
     HIP_TRY(hipGetLastError());
@@ -1418,6 +1454,9 @@ wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t n
 wgrt_status wgrt_selftest_math(const double *a, const double *b, int64_t n, double *out, void *stream) {
     if (n > 0 && (!a || !b || !out)) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
     if (n <= 0) return WGRT_OK;
+    int sdev = 0;
+    HIP_TRY(stream_device(stream, &sdev));
+    DEVICE_SCOPE(dev_scope, sdev);
     const int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(selftest_math_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, a, b,
                        n, out);
@@ -1482,7 +1521,7 @@ wgrt_status wgrt_debug_scene_copy(const wgrt_scene *s, int which, void *dst, int
         default: return fail(WGRT_ERR_INVALID_ARGUMENT, "which: 0 cells, 1 tiles, 2 jtiles");
     }
     if (bytes != (int64_t)n) return fail(WGRT_ERR_INVALID_ARGUMENT, "bytes must be " + std::to_string(n));
-    HIP_TRY(hipSetDevice(s->device));
+    DEVICE_SCOPE(dev_scope, s->device);
     HIP_TRY(hipMemcpy(dst, src, n, hipMemcpyDeviceToHost));
     return WGRT_OK;
 }

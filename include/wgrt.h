@@ -26,6 +26,13 @@
  *
  * All pointers passed to wgrt_trace_* are DEVICE pointers (hipMalloc'd or torch
  * ROCm tensors); all pointers in wgrt_scene_desc are HOST pointers.
+ *
+ * Devices: a scene lives on the HIP device it was created on.  Every entry point
+ * that takes a scene allocates and launches on that device, and every entry point
+ * leaves the calling thread's current device (hipGetDevice) as it found it, so one
+ * host thread may drive scenes on several GPUs.  wgrt_rays_init and
+ * wgrt_selftest_math launch on their stream's device (the current one for the null
+ * stream).  A stream passed with a scene must belong to the scene's device.
  */
 #ifndef WGRT_H
 #define WGRT_H

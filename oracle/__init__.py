@@ -49,6 +49,8 @@ class _Rays(ctypes.Structure):
 
 
 _lib = None
+_lib_ev = None
+LIB_EV_PATH = os.path.join(HERE, "build", "libwgrt_oracle_ev.so")
 
 
 def build(quiet: bool = True) -> str:
@@ -59,29 +61,43 @@ def build(quiet: bool = True) -> str:
     return LIB_PATH
 
 
-def lib():
-    global _lib
+def lib(counting: bool = False):
+    """The oracle library; ``counting``: its build with the interaction counter
+    (oracle/wgrt_oracle_ev.c, ``wgrt_oracle_ev_interactions``)."""
+    global _lib, _lib_ev
+    if counting:
+        if _lib_ev is None:
+            if not os.path.exists(LIB_EV_PATH):
+                build()
+            _lib_ev = _declare(ctypes.CDLL(LIB_EV_PATH))
+            _lib_ev.wgrt_oracle_ev_interactions.restype = ctypes.c_int64
+            _lib_ev.wgrt_oracle_ev_interactions.argtypes = [ctypes.c_int]
+        return _lib_ev
     if _lib is None:
         if not os.path.exists(LIB_PATH):
             build()
-        L = ctypes.CDLL(LIB_PATH)
-        L.wgrt_oracle_trace.restype = ctypes.c_int64
-        L.wgrt_oracle_trace.argtypes = [ctypes.POINTER(_Scene), ctypes.POINTER(_Rays), ctypes.c_int64,
-                                        ctypes.c_int64, _u32p, _f32p, _u32p, ctypes.POINTER(ctypes.c_uint8),
-                                        ctypes.c_int]
-        L.wgrt_oracle_hypot.restype = ctypes.c_double
-        L.wgrt_oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
-        L.wgrt_oracle_wrap.restype = ctypes.c_double
-        L.wgrt_oracle_wrap.argtypes = [ctypes.c_double]
-        L.wgrt_oracle_inside.restype = ctypes.c_int
-        L.wgrt_oracle_inside.argtypes = [ctypes.c_double, ctypes.c_double, _f64p, ctypes.c_int64]
-        L.wgrt_oracle_xorshift.restype = ctypes.c_uint32
-        L.wgrt_oracle_xorshift.argtypes = [ctypes.c_uint32, ctypes.c_int64, _f64p]
-        L.wgrt_oracle_inside_many.restype = None
-        L.wgrt_oracle_inside_many.argtypes = [_f64p, ctypes.c_int64, _f64p, ctypes.c_int64,
-                                              ctypes.POINTER(ctypes.c_int32)]
-        _lib = L
+        _lib = _declare(ctypes.CDLL(LIB_PATH))
     return _lib
+
+
+def _declare(L):
+    """ctypes signatures of the oracle library L."""
+    L.wgrt_oracle_trace.restype = ctypes.c_int64
+    L.wgrt_oracle_trace.argtypes = [ctypes.POINTER(_Scene), ctypes.POINTER(_Rays), ctypes.c_int64,
+                                    ctypes.c_int64, _u32p, _f32p, _u32p, ctypes.POINTER(ctypes.c_uint8),
+                                    ctypes.c_int]
+    L.wgrt_oracle_hypot.restype = ctypes.c_double
+    L.wgrt_oracle_hypot.argtypes = [ctypes.c_double, ctypes.c_double]
+    L.wgrt_oracle_wrap.restype = ctypes.c_double
+    L.wgrt_oracle_wrap.argtypes = [ctypes.c_double]
+    L.wgrt_oracle_inside.restype = ctypes.c_int
+    L.wgrt_oracle_inside.argtypes = [ctypes.c_double, ctypes.c_double, _f64p, ctypes.c_int64]
+    L.wgrt_oracle_xorshift.restype = ctypes.c_uint32
+    L.wgrt_oracle_xorshift.argtypes = [ctypes.c_uint32, ctypes.c_int64, _f64p]
+    L.wgrt_oracle_inside_many.restype = None
+    L.wgrt_oracle_inside_many.argtypes = [_f64p, ctypes.c_int64, _f64p, ctypes.c_int64,
+                                          ctypes.POINTER(ctypes.c_int32)]
+    return L
 
 
 def inside_many(points: np.ndarray, poly: np.ndarray) -> np.ndarray:
@@ -156,11 +172,14 @@ class OracleScene:
         return (self.num_lmd, self.ny, self.nx, 80, 120)
 
     def trace(self, rays: dict, rng: np.ndarray, eb: np.ndarray, gid_offset: int = 0,
-              threads: int = 0, per_ray_bounces: bool = False, fate: bool = False):
+              threads: int = 0, per_ray_bounces: bool = False, fate: bool = False,
+              interactions: bool = False):
         """One launch over the shard ``rays`` (mutates ``rng`` and ``eb``).
 
         Returns ``(total_bounces, per_ray_counts_or_None)``, plus the per-ray fate codes
-        when ``fate`` is set."""
+        when ``fate`` is set, plus (last) the launch's coupler interactions -- the Monte-Carlo
+        draws after the in-coupling event, counted by the oracle's event-hook build -- when
+        ``interactions`` is set."""
         cols = {k: np.ascontiguousarray(rays[src], dtype=np.float32) for k, src in
                 (("x", "x"), ("y", "y"), ("m", "m"), ("n", "n"), ("lmd", "lmd_num"), ("te", "te"),
                  ("tm", "tm"), ("dph", "delta_phase")) if not (self.single_lambda and k == "lmd")}
@@ -171,9 +190,13 @@ class OracleScene:
                     for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")])
         counts = np.zeros(N, dtype=np.uint32) if per_ray_bounces else None
         fates = np.zeros(N, dtype=np.uint8) if fate else None
-        tot = lib().wgrt_oracle_trace(ctypes.byref(self._s), ctypes.byref(r), N, int(gid_offset),
-                                      _p(rng, _u32p), _p(eb, _f32p),
-                                      _p(counts, _u32p) if counts is not None else None,
-                                      fates.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if fate else None,
-                                      int(threads))
-        return (int(tot), counts, fates) if fate else (int(tot), counts)
+        L = lib(counting=interactions)
+        if interactions:
+            L.wgrt_oracle_ev_interactions(1)
+        tot = L.wgrt_oracle_trace(ctypes.byref(self._s), ctypes.byref(r), N, int(gid_offset),
+                                  _p(rng, _u32p), _p(eb, _f32p),
+                                  _p(counts, _u32p) if counts is not None else None,
+                                  fates.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if fate else None,
+                                  int(threads))
+        out = (int(tot), counts) + ((fates,) if fate else ())
+        return out + ((int(L.wgrt_oracle_ev_interactions(1)),) if interactions else ())

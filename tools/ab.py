@@ -1,6 +1,6 @@
 #!/usr/bin/env python3
 """A/B timing of library builds (exp_libs/<name>/libwgrt.so, tools/ab_build.py) on the bench
-workload: rounds of one subprocess per build (WGRT_LIB), interleaved, each timing `--launches`
+workload: rounds of one subprocess per build (tools/with_lib.py), interleaved, each timing `--launches`
 single-trace launches and one fused `--fused`-trace call with HIP events; prints the per-build
 medians.  Usage: python tools/ab.py NAME [NAME ...] [--rounds 4] [--config C3]"""
 import argparse
@@ -100,9 +100,10 @@ def main():
             launch_kw = {k: num(v) for k, v in (kv.split("=") for kv in lopts.split(",") if kv)}
             lib = os.path.join(REPO, "exp_libs", build, "libwgrt.so") if build != "tree" else ""
             env = dict(os.environ, REPO=REPO, AB_CONFIG=a.config, AB_LAUNCHES=str(a.launches),
-                       AB_FUSED=str(a.fused), WGRT_LIB=lib, AB_ORDER=order, AB_SCENE=json.dumps(scene_kw),
+                       AB_FUSED=str(a.fused), AB_ORDER=order, AB_SCENE=json.dumps(scene_kw),
                        AB_LAUNCH=json.dumps(launch_kw), AB_PROFILE=a.profile, AB_SHARD=str(a.shard))
-            p = subprocess.run([sys.executable, "-c", CHILD], env=env, capture_output=True, text=True, timeout=300)
+            p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "with_lib.py"), lib, "--abi", "4,5", "-c",
+                                CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(p.stderr[-3000:])
                 sys.exit(p.returncode)

@@ -9,9 +9,9 @@ export TMPDIR=/tmp
 timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 --timeout-method thread > "$OUT/${TAG}_pytest.log" 2>&1
 rc=$?; echo "pytest rc $rc"; tail -3 "$OUT/${TAG}_pytest.log"
 if [ $rc -ne 0 ]; then exit $rc; fi
-# PARITY="name ...": the same tests on exp_libs builds (WGRT_LIB)
+# PARITY="name ...": the same tests on exp_libs builds (tools/with_lib.py)
 for v in $PARITY; do
-  WGRT_LIB=$(pwd)/exp_libs/$v/libwgrt.so timeout -k 10 600 python -u -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 \
+  timeout -k 10 600 python -u tools/with_lib.py $(pwd)/exp_libs/$v/libwgrt.so -m pytest ${TESTS:-tests} -m gpu -x -q --timeout 240 \
     --timeout-method thread > "$OUT/${TAG}_pytest_$v.log" 2>&1
   rc=$?; echo "pytest $v rc $rc"; tail -2 "$OUT/${TAG}_pytest_$v.log"
   if [ $rc -ne 0 ]; then exit $rc; fi

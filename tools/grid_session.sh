@@ -13,7 +13,7 @@ timeout -k 10 300 python tools/ab.py $NAMES --rounds 3 --config C2 --fused 4 > $
 grep SUMMARY $O/${TAG}_ab_C2.log
 for v in $NAMES; do
   for n in 2 4 8; do
-    WGRT_LIB=$(pwd)/exp_libs/$v/libwgrt.so timeout -k 10 200 python bench.py --emulate-ranks $n --steps 10 --warmup 2 \
+    timeout -k 10 200 python tools/with_lib.py $(pwd)/exp_libs/$v/libwgrt.so bench.py --emulate-ranks $n --steps 10 --warmup 2 \
       > $O/${TAG}_em_${v}_$n.log 2>&1 || exit $?
     echo "$v N=$n $(grep -o '"predicted_ms_per_step": [0-9.]*' $O/${TAG}_em_${v}_$n.log)"
   done

@@ -4,7 +4,10 @@
 Runs the bench workload (C3 by default), records per wave: start, queue-exhausted and end
 times, passes and lane-passes, and prints a summary: launch span, when the work queue ran dry,
 the drain (tail) after it, lane occupancy before and after, per-XCD end times.
-Usage: python tools/timeline.py [--config C3] [--num-iter 1] [--variant 0] [--out FILE]
+Usage: python tools/timeline.py [--config C3] [--num-iter 1] [--variant 0] [--shard N] [--out FILE]
+--shard N: rank 0's interleaved FoV x wavelength shard of N (distributed.make_shard), i.e. what one GPU
+of the N-GPU strong-scaling run traces.  Single traces use the product's grid rule (wgrt_launch_opts
+grid_sqrt_k: ceil(6.5 sqrt(work items)) workgroups), like the launches the bench times.
 """
 import argparse
 import ctypes
@@ -28,6 +31,7 @@ def main():
     ap.add_argument("--raw", default=None, help="also save the per-wave records (npz)")
     ap.add_argument("--order", default="none", choices=["none", "lifetime"],
                     help="chunk issue order: ascending, or long-lived tiles first (from a previous launch)")
+    ap.add_argument("--shard", type=int, default=1, help="trace rank 0's interleaved shard of N ranks")
     a = ap.parse_args()
     import torch
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS, build_inputs
@@ -39,17 +43,21 @@ def main():
     nx, ny, lam, R = w.nx, w.ny, list(w.lambdas), w.R
     geom, luts, pts = build_inputs(w)
     scene = Scene.from_geometry(geom, luts)
-    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(make_shard(nx, ny, len(lam), R, 1, 0))
+    shard = make_shard(nx, ny, len(lam), R, a.shard, 0)
+    rays, rng = hip_shard_builder(pts, nx, ny, lam, R, dev)(shard)
+    gkw = {} if a.shard == 1 else dict(gid_blocks=torch.as_tensor(shard.gid.block_gid, dtype=torch.int64, device=dev),
+                                       gid_block_rays=R)
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     nw = 256 * 8 * 4 * 2
     buf = torch.zeros(8 * nw, dtype=torch.int64, device=dev)
     order = None
     if a.order == "lifetime":
         per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
-        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, per_ray_bounces=per)
+        trace_fullcolor(scene, rays, rng, eb, variant=a.variant, per_ray_bounces=per, **gkw)
         tile = ((rays["lmd_num"].long() * nx + rays["m"].long()) * ny + rays["n"].long())
         order = schedule_by_lifetime(per, tile, len(lam) * nx * ny)
     kw = dict(chunk_order=order) if order is not None else {}
+    kw.update(gkw)
     for _ in range(2):
         trace_fullcolor(scene, rays, rng, eb, variant=a.variant, num_iter=a.num_iter, **kw)
     res = []
@@ -88,11 +96,18 @@ def main():
             np.savez_compressed(f"{a.raw}.{rep}.npz", start=start, exh=exh, end=end, passes=passes, lanes=lanes,
                                 xcc=xcc, p_exh=p_exh, l_exh=l_exh)
         r["order"] = a.order
+        r["workgroups"] = int(len(t)) // 4
+        r["rays"] = int(rng.numel())
         res.append(r)
         print(json.dumps(r), flush=True)
     if a.out:
         with open(a.out, "w") as f:
-            json.dump({"config": a.config, "num_iter": a.num_iter, "runs": res}, f, indent=1)
+            import hashlib
+            from gpu_ray_tracing_for_waveguide_based_ar_display_amd._lib import loaded_path
+            with open(loaded_path(), "rb") as lf:
+                sha = hashlib.sha256(lf.read()).hexdigest()[:16]
+            json.dump({"config": a.config, "num_iter": a.num_iter, "shard_of": a.shard, "lib_sha16": sha,
+                       "runs": res}, f, indent=1)
 
 
 if __name__ == "__main__":
