@@ -10,7 +10,6 @@ a second device the scene is also created on it while device 0 stays current.
 
 Tolerance: exact (device ordinals; the trace's results are compared with the golden fixture)."""
 import ctypes
-import os
 
 import numpy as np
 import pytest
@@ -23,7 +22,13 @@ pytestmark = pytest.mark.gpu
 def hip():
     if not torch.cuda.is_available():
         pytest.skip("no HIP device")
-    L = ctypes.CDLL(os.path.join(os.environ.get("ROCM_PATH", "/opt/rocm"), "lib", "libamdhip64.so"))
+    torch.cuda.init()
+    # the HIP runtime this process already runs (torch's copy, which libwgrt.so binds too): loading
+    # another libamdhip64 next to it would not see this process's device selection
+    with open("/proc/self/maps") as f:
+        paths = sorted({ln.split()[-1] for ln in f if "libamdhip64.so" in ln})
+    assert paths, "no HIP runtime mapped"
+    L = ctypes.CDLL(paths[0])
     L.hipGetDevice.argtypes = [ctypes.POINTER(ctypes.c_int)]
     L.hipSetDevice.argtypes = [ctypes.c_int]
 
