@@ -901,40 +901,12 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-#ifdef WGRT_SMEM_HDR
-    // The tile header (moves, hop phasors, cos(ic1 angle), phase growth) is the same for every lane
-    // of a wave whose interacting lanes share one tile -- the usual case: a wave's rays come from
-    // its current 64-ray chunk, and 16 consecutive chunks are one C3 tile.  Such a wave reads the
-    // header with two scalar loads (the scalar cache; no vector-memory instruction, which costs the
-    // CU's load path ~30 cycles however few lanes it serves) and selects per lane; a mixed wave
-    // loads it per lane.
-    const uint32_t tix0 = __builtin_amdgcn_readfirstlane(L.tix);
-    const bool hdr_uni = __builtin_amdgcn_ballot_w64(L.tix != tix0) == 0ull;
-    double2 cg, mva, mvb, hop0, hop1;
-    if (hdr_uni) {
-        typedef const double __attribute__((address_space(4))) CD;
-        CD *Hs = (CD *)(uintptr_t)(KA(jtiles) + (size_t)tix0 * (size_t)A.jtile_d);
-        const double2 g0{Hs[kJGap + 0], Hs[kJGap + 1]}, g2{Hs[kJGap + 2], Hs[kJGap + 3]};
-        const double2 g4{Hs[kJGap + 4], Hs[kJGap + 5]}, g6{Hs[kJGap + 6], Hs[kJGap + 7]};
-        hop0 = double2{Hs[kJHop + 0], Hs[kJHop + 1]};
-        hop1 = double2{Hs[kJHop + 2], Hs[kJHop + 3]};
-        cg = double2{Hs[kJCosIc1], Hs[kJGrowth]};
-        mva = kind >= 3 ? g2 : g0;
-        mvb = kind == 0 ? g4 : (kind >= 3 ? g6 : g2);
-    } else {
-        cg = *(const double2 *)(T + kJCosIc1);
-        mva = *(const double2 *)(T + kJGap + ga);
-        mvb = *(const double2 *)(T + kJGap + gb);
-    }
-    const double4 cw = block_cw(B);
-#else
     const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
     const double4 cw = block_cw(B);
     // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
     // issued together with its matrix, one memory round trip per interaction less
     const double2 mva = *(const double2 *)(T + kJGap + ga);
     const double2 mvb = *(const double2 *)(T + kJGap + gb);
-#endif
     const double denom = entry ? cg.x : r.cos_t;
     const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
     const double inv = rcp_nr(denom);
@@ -965,14 +937,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     L.pf = locate_c(loc, r.x, r.y);
     // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
     // in-coupler states and R5 never hop), loaded with the taken branch's matrix
-    const bool hop_r2 = kind == 0 || (kind <= 2 && ba);
-#ifdef WGRT_SMEM_HDR
-    double2 hop;
-    if (hdr_uni) hop = hop_r2 ? hop0 : hop1;
-    else hop = *(const double2 *)(T + kJHop + (hop_r2 ? 0 : 2));
-#else
-    const double2 hop = *(const double2 *)(T + kJHop + (hop_r2 ? 0 : 2));
-#endif
+    const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
