@@ -54,6 +54,14 @@ HBM_PEAK_GBPS = 8000.0          # MI355X_MICROARCH.md: HBM3E 8.0 TB/s
 LIFETIME_BUCKETS = (1, 10, 30, 100, 300, 1000)   # bounce-count histogram edges (last bucket open)
 LONG_STEPS = 200                # long_region: >= 50 ms of C3 single launches
 EMULATE_STEPS = 20              # single launches per shard in the emulated_strong record
+# emulated_strong: BASELINE configs 3 and 4, and config 5 on the design geometry (C5d) and as the
+# short-hop stress batch (C5, fewer launches: 60 ms each on one GPU)
+EMULATE_CONFIGS = (("C3", EMULATE_STEPS), ("C4", EMULATE_STEPS), ("C5d", EMULATE_STEPS), ("C5", 4))
+# the strong-scaling gather's transfer, modelled: every rank sends its payload (1/N of the eyebox grid) to
+# rank 0 over its own xGMI link at the same time; one direction of a link carries half of the
+# ~153.6 GB/s per-link figure of the node, and one RCCL gather call adds a fixed cost
+XGMI_LINK_GBPS = 76.8
+RCCL_CALL_MS = 0.03
 
 
 def parse(argv=None):
@@ -233,6 +241,9 @@ def main(argv=None):
     elapsed, bounces_total, bounces_local, _ = timed(a.steps, 1, events=False)
     value = bounces_total / elapsed
     _el, _bt, ev_bounces_local, call_ms = timed(a.steps, 1)
+    binding = None
+    if world == 1 and cname == "C3" and shard.n_rays and a.variant in (0, 7):
+        binding = binding_record(scene, rays, rng, eb, shard, R, dev, lifetimes)
     extras = {}
     if not a.no_extras:
         for key, steps, note in (("main_job", 4, "the reference's job: 4 chained traces (MAIN:169-177) as one call, "
@@ -265,8 +276,7 @@ def main(argv=None):
             del wr, wg
     emulated = None
     if world == 1 and not a.no_extras and cname == "C3":
-        emulated = emulated_strong(a, scene, dev, elapsed / a.steps * 1e3,
-                                   extras.get("main_job", {}).get("ms_per_step"))
+        emulated = emulated_strong(a, scene, dev)
 
     if rank == 0:
         kavg_s = float(np.mean(call_ms)) / 1e3
@@ -302,6 +312,7 @@ def main(argv=None):
                     "bounces_per_launch": int(round(bpl)),
                     "valu": valu if valu is not None else {
                         "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
+                    "binding": binding,
                     "note": "achieved = algorithmic bytes (72 B x bounces) / launch_avg_ms; launch_avg_ms: HIP events "
                             "around each launch (trace kernel + its eyebox/replay epilogue kernel) on rank 0, in a "
                             "second pass of the same K launches (the timed steps carry no event records); valu: the "
@@ -327,7 +338,10 @@ def main(argv=None):
                        "rays_rank0": shard.n_rays,
                        "lut": f"synthetic seed {a.lut_seed} profile {w.profile}", "gap_scale": w.gap_scale,
                        "parallelism": par, "kernel_variant": a.variant, "steps_per_launch": 1, "lib_sha16": sha,
-                       "scene_create_s": round(t_scene, 3), "lifetimes_rank0": lifetimes},
+                       "scene_create_s": round(t_scene, 3), "lifetimes_rank0": lifetimes,
+                       "lut_staging": ("BASELINE config 3 names LUT tiles staged in LDS: built and measured "
+                                       "slower (single launch +28-37 %, DESIGN.md §5.4), so the tiles are read "
+                                       "through L1/L2 and what runs is not LDS-staged")},
             "roofline": roofline,
             "main_job": extras.get("main_job"),
             "fused": extras.get("fused"),
@@ -342,11 +356,41 @@ def main(argv=None):
         dist.destroy_process_group()
 
 
+def binding_record(scene, rays, rng, eb, shard, R, dev, lifetimes):
+    """What bounds the headline launch, measured on it: one more (untimed) launch of the same batch
+    through the wave-timeline instantiation of the same trace kernel (wgrt_debug_opts.timeline): when
+    the work queue ran dry, when the last wave ended, and the pass durations before and after.  The
+    kernel is not bound by the HBM roof the north star names (``frac``): a launch is its bulk --
+    every lane busy, paced by the CU's load path serving the lanes' dependent gathers -- plus the
+    drain of its longest ray chains, each bounce a chain of dependent loads (cell word -> block
+    line -> taken matrix) and ~600 instructions per wave pass."""
+    import torch
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import timeline_summary, trace_fullcolor
+    buf = torch.zeros(8 * 256 * 8 * 4 * 2, dtype=torch.int64, device=dev)
+    g = shard.gid
+    kw = dict(gid_offset=g.offset) if g.offset is not None else dict(gid_blocks=g.device_blocks(dev),
+                                                                     gid_block_rays=R)
+    trace_fullcolor(scene, rays, rng, eb, variant=7, debug=dict(timeline=buf), **kw)
+    torch.cuda.synchronize()
+    t = timeline_summary(buf)
+    chain = lifetimes.get("max", 0) * t["drain_us_per_pass"]
+    return {"limit": "dependent-gather chain: bulk paced by the CU load path, then the drain of the longest ray "
+                     "chains", **t,
+            "longest_ray_bounces": lifetimes.get("max"),
+            "longest_chain_us_at_drain_pass": round(chain, 1),
+            "note": "one untimed launch of the headline batch through the timeline instantiation of the trace "
+                    "kernel (s_memrealtime per wave; the instrumented launch runs ~10 % slower): drain_frac = "
+                    "(last wave end - median queue-dry time) / last wave end; the HBM frac above is the north "
+                    "star's reporting roof, not the binding one"}
+
+
 def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="interleaved"):
     """Each of the N strong-scaling shards of workload w (distributed.make_shard) traced alone on this
     GPU: ``steps`` single launches (HIP events around them) and one 4-chained call (the reference's
     job shape, MAIN:169-177, one persistent launch).  Returns the per-rank ms per step and the
-    predicted N-GPU step time = the slowest shard's (the eyebox collective not included)."""
+    predicted N-GPU step time = the slowest shard's (the eyebox collective not included: see
+    collective_cost)."""
     import torch
 
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
@@ -392,37 +436,89 @@ def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="i
                     "without the eyebox collective"}
 
 
-def emulated_strong(a, scene, dev, ms_one, job_ms_one):
-    """The N = 2 / 4 / 8 strong-scaling curve of C3 (this scene) and C4 predicted on one GPU
-    (emulate_shards): per N the slowest shard's ms per step and the speedup over one GPU, for single
-    launches and for the reference's 4-chained job."""
+def collective_cost(scene, w, N, dev, assign="interleaved", reps=10):
+    """The strong-scaling eyebox gather at N ranks (distributed.EyeboxGather) on this GPU: the device
+    time of one rank's pack (the largest shard's) and of rank 0's assembly of all N payloads, with the
+    reused buffers of the collective (HIP events, median of ``reps``), plus the modelled transfer
+    (every rank's payload over its own xGMI link at once, XGMI_LINK_GBPS, plus RCCL_CALL_MS)."""
+    import torch
+
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import EyeboxGather, make_shard
+    nx, ny, lambdas, R = w.nx, w.ny, list(w.lambdas), w.R
+    blocks = [make_shard(nx, ny, len(lambdas), R, N, r, assign).blocks for r in range(N)]
+    g = EyeboxGather(blocks, nx, ny, lambdas, scene.num_lmd, device=dev)
+    gen = torch.Generator(device=dev)
+    gen.manual_seed(N)
+    eb = torch.randint(0, 4, scene.eb_shape(), generator=gen, device=dev).to(torch.float32)
+    out = torch.empty_like(eb)
+    send, recv = g.buffers(dev, eb.dtype, True)
+    for r in range(N):
+        g.pack(eb, r, out=recv[r])
+    big = max(range(N), key=lambda r: g.counts[r])
+
+    def med(fn):
+        ts = []
+        for _ in range(reps):
+            t0, t1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            t0.record()
+            fn()
+            t1.record()
+            torch.cuda.synchronize()
+            ts.append(t0.elapsed_time(t1))
+        return float(np.median(ts))
+
+    fn_pack = lambda: g.pack(eb, big, out=send)
+    fn_asm = lambda: g.assemble(out, [recv[r] for r in range(N)])
+    fn_pack()
+    fn_asm()
+    pack_ms, asm_ms = med(fn_pack), med(fn_asm)
+    payload = g.payload_len * 4
+    xfer_ms = payload / (XGMI_LINK_GBPS * 1e9) * 1e3 + RCCL_CALL_MS
+    return {"pack_ms": round(pack_ms, 4), "assemble_ms": round(asm_ms, 4), "payload_bytes_per_rank": payload,
+            "xfer_ms_modelled": round(xfer_ms, 4), "total_ms": round(pack_ms + asm_ms + xfer_ms, 4)}
+
+
+def emulated_strong(a, scene, dev):
+    """The N = 2 / 4 / 8 strong-scaling curve of EMULATE_CONFIGS predicted on one GPU: per N the
+    slowest shard's ms per step (emulate_shards, the same event-timed method as the one-GPU
+    baseline beside it) and the speedup over one GPU, for single launches and for the reference's
+    4-chained job; then the same with the eyebox gather included (collective_cost, once per timed
+    region of a.steps steps, and once per 4-trace job)."""
     import torch
 
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.configs import CONFIGS, build_inputs
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene
-    steps = min(a.steps, EMULATE_STEPS)
     out = {}
-    for cname in ("C3", "C4"):
+    K = max(a.steps, 1)
+    for cname, nsteps in EMULATE_CONFIGS:
+        steps = min(a.steps, nsteps)
         w = CONFIGS[cname]
         geom, luts, points = build_inputs(w, lut_seed=a.lut_seed)
         sc = scene if cname == "C3" else Scene.from_geometry(geom, luts, device=dev.index or 0)
-        one, one_job = ms_one, job_ms_one
-        if cname != "C3":   # C4 on one GPU: the same measurement as the shards'
-            whole = emulate_shards(sc, w, points, 1, steps, 2, dev, a.variant, a.assign)
-            one, one_job = whole["predicted_ms_per_step"], whole["predicted_job_ms_per_step"]
-        rec = {"one_gpu_ms_per_step": round(one, 4), "one_gpu_job_ms_per_step": one_job}
+        whole = emulate_shards(sc, w, points, 1, steps, 2, dev, a.variant, a.assign)
+        one, one_job = whole["predicted_ms_per_step"], whole["predicted_job_ms_per_step"]
+        rec = {"one_gpu_ms_per_step": round(one, 4), "one_gpu_job_ms_per_step": one_job, "steps": steps}
         for n in (2, 4, 8):
             e = emulate_shards(sc, w, points, n, steps, 2, dev, a.variant, a.assign)
-            rec[str(n)] = {"ms_per_step": e["predicted_ms_per_step"], "speedup": round(one / e["predicted_ms_per_step"], 3),
-                           "value": e["predicted_value"], "job_ms_per_step": e["predicted_job_ms_per_step"],
-                           "job_speedup": (round(one_job / e["predicted_job_ms_per_step"], 3) if one_job else None)}
+            c = collective_cost(sc, w, n, dev, a.assign)
+            ms, job = e["predicted_ms_per_step"], e["predicted_job_ms_per_step"]
+            ms_c, job_c = ms + c["total_ms"] / K, job + c["total_ms"] / 4
+            rec[str(n)] = {"ms_per_step": ms, "speedup": round(one / ms, 3), "value": e["predicted_value"],
+                           "job_ms_per_step": job, "job_speedup": round(one_job / job, 3),
+                           "collective": c,
+                           "with_collective": {"ms_per_step": round(ms_c, 4), "speedup": round(one / ms_c, 3),
+                                               "job_ms_per_step": round(job_c, 4),
+                                               "job_speedup": round(one_job / job_c, 3)}}
         if sc is not scene:
             sc.close()
         out[cname] = rec
         torch.cuda.synchronize()
     out["note"] = ("strong scaling predicted on one MI355X: each of the N interleaved FoV x lambda shards "
-                   "(bench.py --gpus N --scaling strong) traced alone, the slowest one's step time; single "
-                   "launches and the reference's 4-chained job per shard; without the eyebox gather")
+                   "(bench.py --gpus N --scaling strong) traced alone, the slowest one's step time (HIP events, "
+                   "the same method for the one-GPU baseline); single launches and the reference's 4-chained job "
+                   "per shard.  with_collective adds the eyebox gather: pack and rank-0 assembly timed on this "
+                   f"GPU, the transfer modelled at {XGMI_LINK_GBPS} GB/s per xGMI link plus {RCCL_CALL_MS} ms per "
+                   f"call; once per timed region of {K} steps for single launches, once per 4-trace job")
     return out
 
 

@@ -220,61 +220,102 @@ class EyeboxGather:
     """Gather of each rank's own eyebox slabs (+ their spill) to rank 0, and the assembly there.
 
     ``all_blocks[r]``: global block ids of rank r (every rank knows the whole assignment, so
-    the message sizes and placements need no exchange).  The payload is padded to the largest
-    shard, as the collective needs equal sizes."""
+    the message sizes and placements need no exchange).  A rank's payload is one flat buffer,
+    ``[nb x 9600 slab floats | nb x SPILL spill floats]``, padded to the largest shard (the
+    collective needs equal sizes).  The send buffer and rank 0's receive buffers are allocated once
+    (first call per device and dtype) and reused; pack and assembly are device-side gathers and
+    scatters with every index precomputed on the host here, so a call makes no host round trip
+    before the collective.  The assembly writes each owned slab once, from the rank that traced it
+    (one ``index_copy_`` per rank), zeroes only slabs no rank owns, and adds the spills."""
 
     def __init__(self, all_blocks, num_fov_x: int, num_fov_y: int, lambdas, n_lambda_scene: int, device=None):
         import torch
         self.n_slabs = n_lambda_scene * num_fov_y * num_fov_x
         self.world = len(all_blocks)
         self.nb = max(len(b) for b in all_blocks)
-        self.slabs, self.spill, self.spill_dst = [], [], []
+        self.payload_len = self.nb * (EB_SLAB + SPILL)
+        self.device = device
+        t = lambda a, dt=torch.int64: torch.as_tensor(np.asarray(a), dtype=dt, device=device)
+        self.slabs, self.nxt, self.spill_mask, self.spill_rows, self.spill_dst = [], [], [], [], []
+        self.has_spill, self.counts = [], []
+        owned = np.zeros(self.n_slabs, dtype=bool)
         for b in all_blocks:
             s = slab_ids(b, num_fov_x, num_fov_y, lambdas)
             own = set(s.tolist())
+            owned[s] = True
             # the spill of slab s lands in s + 1; it must travel unless s + 1 is this rank's own
             # slab (then it is already in that slab's copy) or past the grid (dropped, as the
             # kernel's guard drops it)
             sp = np.array([(v + 1) not in own and v + 1 < self.n_slabs for v in s.tolist()], dtype=bool)
-            self.slabs.append(torch.as_tensor(s, dtype=torch.int64, device=device))
-            self.spill.append(torch.as_tensor(sp, device=device))
-            self.spill_dst.append(torch.as_tensor(s[sp] + 1, dtype=torch.int64, device=device))
+            self.counts.append(len(s))
+            self.slabs.append(t(s))
+            self.nxt.append(t(np.minimum(s + 1, self.n_slabs - 1)))
+            self.spill_mask.append(t(sp, torch.float32))
+            self.spill_rows.append(t(np.nonzero(sp)[0]))
+            self.spill_dst.append(t(s[sp] + 1))
+            self.has_spill.append(bool(sp.any()))
+        self.unowned = t(np.nonzero(~owned)[0])
+        self.any_unowned = bool((~owned).any())
+        self._bufs = {}
 
-    def pack(self, eb, rank: int):
+    def buffers(self, device, dtype, dst: bool):
+        """(send, recv): the payload buffer and, on the gathering rank, the [world, payload] receive
+        buffer (None elsewhere); allocated on first use, zeroed once (padding rows stay zero)."""
+        import torch
+        key = (str(device), dtype, dst)
+        if key not in self._bufs:
+            send = torch.zeros(self.payload_len, dtype=dtype, device=device)
+            recv = torch.zeros((self.world, self.payload_len), dtype=dtype, device=device) if dst else None
+            self._bufs[key] = (send, recv)
+        return self._bufs[key]
+
+    def _views(self, buf):
+        nb = self.nb
+        return buf[:nb * EB_SLAB].view(nb, EB_SLAB), buf[nb * EB_SLAB:].view(nb, SPILL)
+
+    def pack(self, eb, rank: int, out=None):
+        """Rank ``rank``'s payload, into ``out`` (the collective passes its reused send buffer) or a new
+        zeroed buffer."""
         import torch
         flat = eb.reshape(self.n_slabs, EB_SLAB)
-        s = self.slabs[rank]
-        out = torch.zeros((self.nb, EB_SLAB + SPILL), dtype=eb.dtype, device=eb.device)
-        out[:len(s), :EB_SLAB] = flat.index_select(0, s)
-        sp = self.spill[rank]
-        if bool(sp.any()):
-            nxt = torch.clamp(s + 1, max=self.n_slabs - 1)
-            out[:len(s), EB_SLAB:] = flat.index_select(0, nxt)[:, :SPILL] * sp[:, None].to(eb.dtype)
-        return out
+        buf = out if out is not None else torch.zeros(self.payload_len, dtype=eb.dtype, device=eb.device)
+        main, spill = self._views(buf)
+        n = self.counts[rank]
+        torch.index_select(flat, 0, self.slabs[rank], out=main[:n])
+        if self.has_spill[rank]:
+            torch.index_select(flat[:, :SPILL], 0, self.nxt[rank], out=spill[:n])
+            spill[:n].mul_(self.spill_mask[rank].to(eb.dtype)[:, None])
+        return buf
 
     def assemble(self, eb, parts) -> None:
-        """Rank 0: rebuild the whole grid in ``eb`` from every rank's packed payload."""
+        """Rank 0: rebuild the whole grid in ``eb`` from every rank's payload (``parts[r]``: rank r's
+        flat payload, e.g. row r of the receive buffer)."""
         flat = eb.reshape(self.n_slabs, EB_SLAB)
-        flat.zero_()
+        if self.any_unowned:
+            flat.index_fill_(0, self.unowned, 0)
         for r, p in enumerate(parts):
-            s = self.slabs[r]
-            flat.index_copy_(0, s, p[:len(s), :EB_SLAB])
+            n = self.counts[r]
+            if n:
+                flat.index_copy_(0, self.slabs[r], self._views(p)[0][:n])
+        head = flat[:, :SPILL]
         for r, p in enumerate(parts):
-            sp = self.spill[r]
-            if len(self.spill_dst[r]):
-                flat[:, :SPILL].index_add_(0, self.spill_dst[r], p[:len(self.slabs[r])][sp][:, EB_SLAB:])
+            if self.has_spill[r]:
+                head.index_add_(0, self.spill_dst[r], self._views(p)[1].index_select(0, self.spill_rows[r]))
 
     def __call__(self, eb, group=None, dst: int = 0):
-        import torch
         import torch.distributed as dist
         if _world(group) <= 1:
             return eb
         rank = dist.get_rank(group)
-        payload = self.pack(eb, rank)
         on_gloo_dev = getattr(eb, "is_cuda", False) and dist.get_backend(group) == "gloo"
+        send, recv = self.buffers(eb.device, eb.dtype, rank == dst)
+        payload = self.pack(eb, rank, out=send)
         if on_gloo_dev:
-            payload = payload.cpu()   # gloo gathers host tensors (the bench's one-GPU rehearsal)
-        parts = [torch.empty_like(payload) for _ in range(self.world)] if rank == dst else None
+            # gloo gathers host tensors (the bench's one-GPU rehearsal)
+            payload = payload.cpu()
+            parts = [recv[r].cpu() for r in range(self.world)] if rank == dst else None
+        else:
+            parts = [recv[r] for r in range(self.world)] if rank == dst else None
         dist.gather(payload, gather_list=parts, dst=dst, group=group)
         if rank == dst:
             self.assemble(eb, [p.to(eb.device) for p in parts] if on_gloo_dev else parts)

@@ -183,6 +183,33 @@ def _trace(scene, rays, rng_states, matrix_EB, gid_offset, n_rays, stats, per_ra
     check(status, "wgrt_trace_single" if single else "wgrt_trace_fullcolor")
 
 
+def timeline_summary(buf, percentiles: bool = True) -> dict:
+    """Summary of one launch's wave timeline (``debug=dict(timeline=buf)``: 8 int64 words per wave --
+    start, queue exhausted, end (s_memrealtime, 100 MHz), passes, lane-passes, XCD, passes and
+    lane-passes up to the queue running dry): when the work queue ran dry, when the waves ended,
+    and the pass durations and lane occupancy before (bulk) and after (drain) -- where a single
+    launch's time goes."""
+    t = buf.cpu().numpy().reshape(-1, 8)
+    t = t[t[:, 0] > 0]
+    start, exh, end, passes, lanes, xcc, p_exh, l_exh = (t[:, k].astype(np.float64) for k in range(8))
+    t0 = start.min()
+    us = lambda v: (v - t0) / 100.0   # 100 MHz ticks -> us
+    drain_passes = passes - p_exh
+    last = us(end) >= np.percentile(us(end), 99)
+    pc = lambda v, qs: [round(float(np.percentile(v, q)), 3) for q in qs]
+    return {"waves": int(len(t)),
+            "exhausted_us": pc(us(exh), (0, 50, 100)),
+            "end_us": pc(us(end), (0, 50, 99, 100)),
+            "drain_frac": round(float((us(end).max() - np.median(us(exh))) / max(us(end).max(), 1e-9)), 4),
+            "bulk_us_per_pass": round(float(np.median(us(exh) / np.maximum(p_exh, 1))), 3),
+            "drain_us_per_pass": round(float(np.median((end - exh) / 100.0 / np.maximum(drain_passes, 1))), 3),
+            "bulk_lanes_per_pass": round(float(l_exh.sum() / max(p_exh.sum(), 1)), 2),
+            "drain_lanes_per_pass": round(float((lanes - l_exh).sum() / max(drain_passes.sum(), 1)), 2),
+            "last1pct_drain_passes": round(float(np.median(drain_passes[last])), 1),
+            "last1pct_drain_us_per_pass": round(float(np.median(((end - exh) / 100.0 /
+                                                                   np.maximum(drain_passes, 1))[last])), 3)}
+
+
 def schedule_by_lifetime(per_ray_bounces, tile_of_ray, n_tiles: int | None = None):
     """Issue order of the 64-ray chunks for ``chunk_order``: the chunks whose rays belong to the
     (wavelength, FoV) tiles with the longest mean lifetime in a previous launch go first, so the

@@ -72,6 +72,23 @@ PROFILES = {
     "balanced": dict(ic=(0.45, 0.45), r0=(0.5, 0.5), r1=(0.5, 0.5),
                      fc_fold=(0.5, 0.5), fc_keep=1.0, fc_back=0.5, fc2_keep=1.0,
                      oc_turn=0.33, oc_out=(0.33, 0.33), oc_keep=1.0),
+    # Adversarial profiles for the Jones lane's certified decisions, where its
+    # bound is weakest:
+    # * near-singular Jones matrices (condition number ~1e6: a rank-one matrix plus 1e-6 of a
+    #   unitary one), so a branch's efficiency depends steeply on the ray's polarisation and the
+    #   carried Jones vector is far from the matrices' well-conditioned directions; targets are the
+    #   default profile's, reached for the most-transmitted polarisation;
+    "adversarial_singular": dict(ic=(0.40, 0.05), r0=(0.85, 0.05), r1=(0.05, 0.85),
+                                 fc_fold=(0.08, 0.30), fc_keep=0.97, fc_back=0.04, fc2_keep=0.93,
+                                 oc_turn=0.03, oc_out=(0.06, 0.25), oc_keep=0.96, jones="singular", cond=1e6),
+    # * lossless interactions whose branch efficiencies sum to 1 - 1e-9 and split (nearly) evenly, no
+    #   jitter: every interaction's last threshold sits 1e-9 below 1 (draws near 1 decide against it)
+    #   and the branch thresholds sit near the common draw 0.5; with shortened hops (tests scale
+    #   lut_gap) rays live for hundreds to thousands of bounces, so the reference's unwrapped phase
+    #   (delta_phase += 2 lut_TIR per miss hop, GRTF:1052, 1108, 1178) grows long.
+    "adversarial_lossless": dict(ic=(0.5, 0.5 - 1e-9), r0=(0.5, 0.5 - 1e-9), r1=(0.5 - 1e-9, 0.5),
+                                 fc_fold=(0.5, 0.5), fc_keep=1.0 - 1e-9, fc_back=0.5, fc2_keep=1.0 - 1e-9,
+                                 oc_turn=1.0 / 3.0, oc_out=(1.0 / 3.0, 1.0 / 3.0), oc_keep=1.0 - 1e-9, jitter=0.0),
 }
 
 
@@ -91,9 +108,33 @@ def _jones(rng, shape, scale):
     return amp * a, amp * b, amp * (-ep * np.conj(b)), amp * (ep * np.conj(a))
 
 
+def _jones_singular(rng, shape, scale, cond):
+    """Random near-singular 2x2 Jones matrices: u v^H + (1 / cond) U (u, v random unit complex
+    vectors, U random unitary), scaled so the largest singular value squared is ``scale`` -- the
+    efficiency of the most-transmitted polarisation -- while the other is ~scale / cond^2."""
+    def unit():
+        th = rng.uniform(0.0, np.pi / 2, shape)
+        p1, p2 = (rng.uniform(-np.pi, np.pi, shape) for _ in range(2))
+        return np.cos(th) * np.exp(1j * p1), np.sin(th) * np.exp(1j * p2)
+    u0, u1 = unit()
+    v0, v1 = unit()
+    e = 1.0 / cond
+    a, b, c, d = _jones(rng, shape, np.ones(shape))
+    m00, m01 = u0 * np.conj(v0) + e * a, u0 * np.conj(v1) + e * b
+    m10, m11 = u1 * np.conj(v0) + e * c, u1 * np.conj(v1) + e * d
+    # largest singular value of [[m00, m01], [m10, m11]]
+    fro = abs(m00) ** 2 + abs(m01) ** 2 + abs(m10) ** 2 + abs(m11) ** 2
+    det = abs(m00 * m11 - m01 * m10)
+    smax2 = 0.5 * (fro + np.sqrt(np.maximum(fro * fro - 4.0 * det * det, 0.0)))
+    amp = np.sqrt(scale / smax2)
+    return amp * m00, amp * m01, amp * m10, amp * m11
+
+
 def synthetic_luts(geom, seed: int = 0, profile: str = "default", jitter: float = 0.25):
     """Seeded synthetic LUT set matching ``geom`` (a :class:`CouplerGeometry`)."""
     tgt = PROFILES[profile]
+    jitter = tgt.get("jitter", jitter)
+    singular = tgt.get("jones") == "singular"
     rng = np.random.default_rng(seed)
     ang = geom.angles
     th_in, th_ic, th_ic2 = ang["th_in_ic"], ang["th_out_ic"], ang["th_out_ic2"]
@@ -111,7 +152,8 @@ def synthetic_luts(geom, seed: int = 0, profile: str = "default", jitter: float 
     def fill(tab, chans, target, ratio):
         shape = tab.shape[:-1]
         eta = target * (1.0 + jitter * rng.uniform(-1.0, 1.0, shape))
-        tete, tmte, tetm, tmtm = _jones(rng, shape, eta / ratio)
+        tete, tmte, tetm, tmtm = (_jones_singular(rng, shape, eta / ratio, tgt["cond"]) if singular else
+                                  _jones(rng, shape, eta / ratio))
         p, q, r, s = chans            # EF(p, q, r, s): Ete' = c_p te + c_r tm; Etm' = c_q te + c_s tm
         tab[..., p] = tete
         tab[..., r] = tmte
