@@ -289,40 +289,18 @@ __device__ __forceinline__ double efield_sq(double Ete, double Etm, double cd, d
     return (a_re * a_re + a_im * a_im) + (c_re * c_re + c_im * c_im);
 }
 
-// The ray's phase difference delta_phase is carried as its phasor (cos, sin)(delta_phase),
-// which is all E_field_cal consumes (GRTF:135: phase = complex(cos(delta), sin(delta))).
-// E_field_cal's output phase wrap(atan2(Etm') - atan2(Ete')) (GRTF:145-150; 0 for a component
-// with |.| < 1e-20) becomes the unit phasor (Etm' / |Etm'|) * conj(Ete' / |Ete'|); adding
-// lut_TIR (a taken branch) or 2 * lut_TIR (a miss hop) becomes a multiplication by its
-// phasor.  The wrap is a no-op for a phasor.  The values equal the reference's cos / sin of
-// the accumulated phase up to last-ulp rounding -- the same order as the 1-ulp differences
-// between the device's and glibc's atan2 / sin / cos that any GPU evaluation of the
-// reference's formula has (tools/math_ulps.py: atan2 differs in 27 % of calls).  A
-// Monte-Carlo decision can change only if a uniform draw lands within ~1e-16 of a branch
-// threshold (about once per 1e8 launches of the C3 batch).
-struct Phasor {
-    double c, s;
-};
-
-__device__ __forceinline__ Phasor mul(const Phasor &a, const Phasor &b) {
-    return Phasor{a.c * b.c - a.s * b.s, a.c * b.s + a.s * b.c};
-}
-
-__device__ __forceinline__ Phasor field_phasor(const Field &f, double te, double tm) {
-    const bool ue = te >= 1e-20, um = tm >= 1e-20;
-    const double er = ue ? f.te_re : 1.0, ei = ue ? f.te_im : 0.0;
-    const double mr = um ? f.tm_re : 1.0, mi = um ? f.tm_im : 0.0;
-    const double den = (ue ? te : 1.0) * (um ? tm : 1.0);
-    // (mr + i mi) * (er - i ei) / (|Etm'| |Ete'|)
-    double inv = __builtin_amdgcn_rcp(den);
-    inv = fma(inv, fma(-den, inv, 1.0), inv);
-    inv = fma(inv, fma(-den, inv, 1.0), inv);
-    return Phasor{(mr * er + mi * ei) * inv, (mi * er - mr * ei) * inv};
-}
-
+// The exact lane carries the ray's delta_phase as the reference does (GRTF:857): a taken branch
+// sets it to E_field_cal's wrapped phase difference plus lut_TIR (GRTF:145-150, 877, 926, ...), a
+// miss hop adds 2 lut_TIR without a wrap (GRTF:1052, 1108, 1178), and every E_field_cal takes
+// cos / sin of the accumulated, unwrapped value (GRTF:135).  The rounding of that accumulation is
+// part of the reference's result: with lut_TIR near +-pi and runs of hundreds of hops the phase
+// reaches thousands of radians, and a rotation carried as a product of hop phasors instead (round
+// 4's lane) drifted from it far enough to change decisions (the adversarial_lossless LUTs of
+// tests/test_gpu_certification.py: 33 of 96,768 rays).  This lane differs from the reference only by
+// the device's cos / sin / atan2 against glibc's (ulps of the result).
 struct Ray {
     double x, y, te, tm, cos_t, ener;
-    Phasor ph;   // (cos, sin) of delta_phase
+    double dph;   // delta_phase (GRTF:857), unwrapped as the reference carries it
     uint32_t s;
     int region;
 };
@@ -352,11 +330,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
     L.r.y = (double)A.y[ld];
     L.r.te = (double)A.te[ld];
     L.r.tm = (double)A.tm[ld];
-    {
-        double sd, cd;
-        sincos((double)A.dph[ld], &sd, &cd);
-        L.r.ph = Phasor{cd, sd};
-    }
+    L.r.dph = (double)A.dph[ld];
     L.r.cos_t = 1.0;
     L.r.ener = 1.0;
     L.r.s = A.rng[ld];
@@ -382,9 +356,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     Ray &r = L.r;
     const double *T = L.T;
     const double *B = T + kTileHeader + kBlock * blk;
-    double sd, cd;
-    cd = r.ph.c;
-    sd = r.ph.s;
+    // phase = complex(math.cos(delta), math.sin(delta)) (GRTF:135), once for every E_field_cal call of
+    // this interaction (they all take the same delta)
+    const double cd = cos(r.dph), sd = sin(r.dph);
     const bool three = kind >= 3;
     const bool thr = kind >= 1;  // the ener > threshold guard exists only in R2..R5
     const double denom = entry ? T[kTileCosIc1] : r.cos_t;
@@ -495,7 +469,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     if (entry) e = e * A.n_g;
     // take the branch (GRTF:872-882 and every branch body after it)
     const double norm = sqrt(cte * cte + ctm * ctm);
-    const Phasor ph = field_phasor(f, cte, ctm);
+    // E_field_cal's output phase (GRTF:145-150): 0 for a component below 1e-20, wrapped difference
+    const double pte = cte >= 1e-20 ? atan2(f.te_im, f.te_re) : 0.0;
+    const double ptm = ctm >= 1e-20 ? atan2(f.tm_im, f.tm_re) : 0.0;
     int tir, gap;
     if (kind == 0) { tir = b == 0 ? 0 : 2; gap = b == 0 ? 0 : 4; }
     else if (kind <= 2) { tir = b == 0 ? 0 : 1; gap = b == 0 ? 0 : 2; }
@@ -503,7 +479,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
     r.cos_t = B[b];
     r.te = cte / norm;
     r.tm = ctm / norm;
-    r.ph = mul(ph, Phasor{T[kTileTirRot + 2 * tir], T[kTileTirRot + 2 * tir + 1]});
+    r.dph = wrap_pi(ptm - pte) + T[kTileTir + tir];   // delta_phase = delta_phase_b + lut_TIR[...] (GRTF:877, ...)
     r.x += T[kTileGap + gap];
     r.y += T[kTileGap + gap + 1];
     r.ener = r.ener * e;
@@ -527,10 +503,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
     const double *T = L.T;
     // A miss hop's step is fixed by the region: R2 moves by gap[0:2] and adds 2*TIR[0],
     // R3 and R4 move by gap[2:4] and add 2*TIR[1] (R5 misses die).  Fetch it once.
-    // (kTileHopRot + g holds the phasor of 2*TIR[g / 2].)
     const int g = (r.region == 2) ? 0 : 2;
     const double gx = T[kTileGap + g], gy = T[kTileGap + g + 1];
-    const Phasor hop{T[kTileHopRot + g], T[kTileHopRot + g + 1]};   // 2 * TIR[g / 2]
+    const double tir2 = 2 * T[kTileTir + g / 2];   // 2*lut_TIR[...] (exact doubling)
     for (;;) {
         if (L.bounces > (uint32_t)kMaxLoop) return kDie;
         ++L.bounces;
@@ -562,7 +537,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const Loc &loc, Lane 
         }
         r.x += gx;
         r.y += gy;
-        r.ph = mul(r.ph, hop);
+        r.dph += tir2;   // delta_phase += 2*lut_TIR[...] (GRTF:1052, 1108, 1178)
     }
 }
 

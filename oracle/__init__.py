@@ -72,6 +72,8 @@ def lib(counting: bool = False):
             _lib_ev = _declare(ctypes.CDLL(LIB_EV_PATH))
             _lib_ev.wgrt_oracle_ev_interactions.restype = ctypes.c_int64
             _lib_ev.wgrt_oracle_ev_interactions.argtypes = [ctypes.c_int]
+            _lib_ev.wgrt_oracle_ev_set_flags.restype = None
+            _lib_ev.wgrt_oracle_ev_set_flags.argtypes = [ctypes.POINTER(ctypes.c_uint8)]
         return _lib_ev
     if _lib is None:
         if not os.path.exists(LIB_PATH):
@@ -173,13 +175,15 @@ class OracleScene:
 
     def trace(self, rays: dict, rng: np.ndarray, eb: np.ndarray, gid_offset: int = 0,
               threads: int = 0, per_ray_bounces: bool = False, fate: bool = False,
-              interactions: bool = False):
+              interactions: bool = False, underflow: bool = False):
         """One launch over the shard ``rays`` (mutates ``rng`` and ``eb``).
 
         Returns ``(total_bounces, per_ray_counts_or_None)``, plus the per-ray fate codes
         when ``fate`` is set, plus (last) the launch's coupler interactions -- the Monte-Carlo
         draws after the in-coupling event, counted by the oracle's event-hook build -- when
-        ``interactions`` is set."""
+        ``interactions`` is set, plus (last) per-ray flags (uint8) of the rays whose trace entered the
+        ener-underflow regime (a guard product ener * e below 2^-1000, oracle/wgrt_oracle_ev.c) when
+        ``underflow`` is set."""
         cols = {k: np.ascontiguousarray(rays[src], dtype=np.float32) for k, src in
                 (("x", "x"), ("y", "y"), ("m", "m"), ("n", "n"), ("lmd", "lmd_num"), ("te", "te"),
                  ("tm", "tm"), ("dph", "delta_phase")) if not (self.single_lambda and k == "lmd")}
@@ -190,13 +194,19 @@ class OracleScene:
                     for k in ("x", "y", "m", "n", "lmd", "te", "tm", "dph")])
         counts = np.zeros(N, dtype=np.uint32) if per_ray_bounces else None
         fates = np.zeros(N, dtype=np.uint8) if fate else None
-        L = lib(counting=interactions)
+        L = lib(counting=interactions or underflow)
         if interactions:
             L.wgrt_oracle_ev_interactions(1)
+        flags = np.zeros(N, dtype=np.uint8) if underflow else None
+        if interactions or underflow:
+            L.wgrt_oracle_ev_set_flags(flags.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if underflow else None)
         tot = L.wgrt_oracle_trace(ctypes.byref(self._s), ctypes.byref(r), N, int(gid_offset),
                                   _p(rng, _u32p), _p(eb, _f32p),
                                   _p(counts, _u32p) if counts is not None else None,
                                   fates.ctypes.data_as(ctypes.POINTER(ctypes.c_uint8)) if fate else None,
                                   int(threads))
         out = (int(tot), counts) + ((fates,) if fate else ())
-        return out + ((int(L.wgrt_oracle_ev_interactions(1)),) if interactions else ())
+        out = out + ((int(L.wgrt_oracle_ev_interactions(1)),) if interactions else ())
+        if underflow:
+            L.wgrt_oracle_ev_set_flags(None)
+        return out + ((flags,) if underflow else ())

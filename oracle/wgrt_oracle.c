@@ -42,6 +42,16 @@
 #ifndef ORACLE_EV
 #define ORACLE_EV(ev, region, x, y, gx, gy) ((void)0)
 #endif
+/* Analysis hooks (oracle/wgrt_oracle_ev.c): every value of the guard product ener * e (GRTF:1020,
+ * 1073, 1136, ...) before it is compared with the threshold, and the start / end of ray i's trace.
+ * No-ops in the oracle library. */
+#ifndef ORACLE_ENER
+#define ORACLE_ENER(en) ((void)0)
+#endif
+#ifndef ORACLE_RAY_BEGIN
+#define ORACLE_RAY_BEGIN(i) ((void)0)
+#define ORACLE_RAY_END(i) ((void)0)
+#endif
 #define EB_NY 80
 #define EB_NX 120
 
@@ -312,6 +322,8 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e1 = (E1.te * E1.te + E1.tm * E1.tm) * lcos(sc, T_FC1, th1) / st.cos_th;
                 double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_FC2, th2) / st.cos_th;
                 double en1 = st.ener * e1, en2 = st.ener * e2;
+                ORACLE_ENER(en1);
+                ORACLE_ENER(en2);
                 double u = rng_draw(&s, gid);
                 ORACLE_EV(0, region, st.x, st.y, 0.0, 0.0);
                 if (u <= e1 && en1 > sc->threshold) {
@@ -374,6 +386,9 @@ static uint32_t trace_one(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
                 double e2 = (E2.te * E2.te + E2.tm * E2.tm) * lcos(sc, T_OC2, th2) / st.cos_th;
                 double e3 = (E3.te * E3.te + E3.tm * E3.tm) * lcos(sc, T_IC1, th_ic1) / st.cos_th / n_g;
                 double en1 = st.ener * e1, en2 = st.ener * e2, en3 = st.ener * e3;
+                ORACLE_ENER(en1);
+                ORACLE_ENER(en2);
+                ORACLE_ENER(en3);
                 double u = rng_draw(&s, gid);
                 ORACLE_EV(0, region, st.x, st.y, 0.0, 0.0);
                 if (u <= e1 && en1 > sc->threshold) {
@@ -424,7 +439,9 @@ int64_t wgrt_oracle_trace(const wgrt_oracle_scene *sc, const wgrt_oracle_rays *r
 #endif
 #pragma omp parallel for schedule(dynamic, 64) reduction(+ : total)
     for (int64_t i = 0; i < n_rays; ++i) {
+        ORACLE_RAY_BEGIN(i);
         uint32_t b = trace_one(sc, rays, i, gid_offset + i, rng, eb, fate_out);
+        ORACLE_RAY_END(i);
         if (bounces_out) bounces_out[i] = b;
         total += b;
     }

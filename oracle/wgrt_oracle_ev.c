@@ -14,7 +14,28 @@ static int64_t oracle_ev_draws;   /* OpenMP threads add with relaxed atomics */
         if ((ev) == 0 && (region) != 9) __atomic_fetch_add(&oracle_ev_draws, 1, __ATOMIC_RELAXED); \
     } while (0)
 
+/* ... and the rays whose trace enters the ener-underflow regime: a guard product ener * e below
+ * 2^-1000, i.e. next to the subnormal range, where whether it rounds to zero (and fails the full-colour
+ * guard ener * e > 0, GRTF:1020) hangs on the last bits of e -- of the libm's cos / sin / atan2.  Such a
+ * ray's path is not determined by the reference's formula alone: a one-ulp change of atan2 or cos moves
+ * it (tests/test_gpu_certification.py). */
+static __thread int oracle_ev_underflow;
+static uint8_t *oracle_ev_flags;
+
+#define ORACLE_ENER(en)                                          \
+    do {                                                         \
+        if ((en) < 0x1p-1000) oracle_ev_underflow = 1;           \
+    } while (0)
+#define ORACLE_RAY_BEGIN(i) (oracle_ev_underflow = 0)
+#define ORACLE_RAY_END(i)                                        \
+    do {                                                         \
+        if (oracle_ev_flags) oracle_ev_flags[i] = (uint8_t)oracle_ev_underflow; \
+    } while (0)
+
 #include "wgrt_oracle.c"
+
+/* Per-ray underflow flags of the next traces go to flags[n_rays] (NULL: not recorded). */
+void wgrt_oracle_ev_set_flags(uint8_t *flags) { oracle_ev_flags = flags; }
 
 /* Interactions counted since the last reset (reset != 0: zero the count after reading it). */
 int64_t wgrt_oracle_ev_interactions(int reset) {

@@ -90,3 +90,20 @@ def test_h6_fixture_exercises_eyebox_aliasing():
             assert row == 0 and fov == n * case.nx + m + 1
         else:
             assert row == 79 and fov == n * case.nx + m
+
+
+def test_event_hook_build_matches_reference(case):
+    """The oracle's event-hook build (oracle/wgrt_oracle_ev.c: interaction counter, ener-underflow
+    flags) is the same arithmetic: bit-exact on the fixtures too, with no ray in the underflow regime
+    and fewer interactions than loop iterations."""
+    sc = OracleScene.from_geometry(case.geom, case.luts, wavelength=case.wavelength)
+    rng = case.fresh_rng()
+    eb = np.zeros(case.eb_shape(), np.float32)
+    tot, per_ray, inter, flags = sc.trace(case.rays, rng, eb, per_ray_bounces=True, interactions=True,
+                                          underflow=True)
+    np.testing.assert_array_equal(per_ray, case.f["bounces"][0])
+    np.testing.assert_array_equal(rng, case.f["rng_after1"])
+    np.testing.assert_array_equal(eb, case.eb_expected(1))
+    traced = int((per_ray > 0).sum())
+    assert 0 <= inter <= tot - traced
+    assert not flags.any()

@@ -1,0 +1,54 @@
+#!/usr/bin/env python3
+"""Round-5 debug: the adversarial lossless/long-phase LUT case (tests/test_gpu_certification.py
+adv_lossless_long) on the exact lane (variant 1), the Jones lane (7, 9; also with raised bounds) and the
+certification shadow, each against the CPU oracle: which rays differ and how."""
+import json
+import sys
+
+import numpy as np
+import torch
+
+sys.path.insert(0, ".")
+from tests.test_gpu_certification import _setup  # noqa: E402
+from oracle import OracleScene  # noqa: E402
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, init_rays, new_stats,  # noqa: E402
+                                                                       shadow, trace_fullcolor)
+from gpu_ray_tracing_for_waveguide_based_ar_display_amd.rays import build_rays, rng_seeds  # noqa: E402
+
+dev = torch.device("cuda", 0)
+nx, ny, lam, R = 9, 7, [0, 1, 2], 512
+prof = sys.argv[1] if len(sys.argv) > 1 else "adversarial_lossless"
+geom, luts, pts = _setup(nx, ny, lam, R, profile=prof, gap_scale=0.05, tir_near_pi=True)
+osc = OracleScene.from_geometry(geom, luts)
+hr = build_rays(pts, nx, ny, lam, R)
+orng = rng_seeds(hr["x"].shape[0])
+oeb = np.zeros(osc.eb_shape(), np.float32)
+tot, cnt, fate = osc.trace(hr, orng, oeb, per_ray_bounces=True, threads=16, fate=True)
+scene = Scene.from_geometry(geom, luts)
+out = {"oracle_total": tot}
+for name, kw in (("v1", dict(variant=1)), ("v7", dict(variant=7)), ("v9", dict(variant=9)),
+                 ("v7_tol1e-6", dict(variant=7, debug=dict(cert_tol=1e-6))),
+                 ("v7_tol32_1e-2", dict(variant=7, debug=dict(cert_tol32=1e-2)))):
+    rays, rng = init_rays(pts, nx, ny, lam, R, device=dev, all_columns=False)
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
+    st = new_stats(dev)
+    trace_fullcolor(scene, rays, rng, eb, per_ray_bounces=per, stats=st, **kw)
+    torch.cuda.synchronize()
+    g = per.cpu().numpy().view(np.uint32)
+    bad = np.nonzero(g != cnt)[0]
+    out[name] = {"mismatch": int(len(bad)), "stats": [int(v) for v in st.cpu()],
+                 "rays": [[int(i), int(g[i]), int(cnt[i]), int(fate[i])] for i in bad[:40]],
+                 "rng_mismatch": int((rng.cpu().numpy().view(np.uint32) != orng).sum()),
+                 "eb_mismatch": int((eb.cpu().numpy() != oeb).sum())}
+    print(name, json.dumps(out[name])[:1500], flush=True)
+rays, rng = init_rays(pts, nx, ny, lam, R, device=dev, all_columns=False)
+per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
+st = shadow(scene, rays, rng, per_ray_bounces=per)
+g = per.cpu().numpy().view(np.uint32)
+bad = np.nonzero(g != cnt)[0]
+out["shadow"] = {"mismatch": int(len(bad)), "rays": [[int(i), int(g[i]), int(cnt[i])] for i in bad[:40]],
+                 "stats": {k: st.get(k) for k in ("decisions", "max_ratio", "max_ratio32", "fallbacks",
+                                                   "uncertain", "silent_flips")}}
+print("shadow", json.dumps(out["shadow"])[:1500], flush=True)
+json.dump(out, open("gpurun_out/r05_adv_debug_%s.json" % prof, "w"), indent=1)
