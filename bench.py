@@ -468,7 +468,7 @@ def collective_cost(scene, w, N, dev, assign="interleaved", reps=10):
         return float(np.median(ts))
 
     fn_pack = lambda: g.pack(eb, big, out=send)
-    fn_asm = lambda: g.assemble(out, [recv[r] for r in range(N)])
+    fn_asm = lambda: g.assemble(out, recv)
     fn_pack()
     fn_asm()
     pack_ms, asm_ms = med(fn_pack), med(fn_asm)

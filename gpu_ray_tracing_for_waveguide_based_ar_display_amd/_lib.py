@@ -17,13 +17,13 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libwgrt.so")   # the in-tree build, the only one the product binds
 OPS_PATH = os.path.join(PKG, "_wgrt_torch.so")   # the torch operator library (csrc/wgrt_torch.cpp)
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 # include/wgrt.h (the drop-in boundary) and include/wgrt_debug.h (test / profiling hooks)
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_create_ex", "wgrt_scene_destroy", "wgrt_scene_get_info",
             "wgrt_trace_fullcolor", "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex",
             "wgrt_trace_opts", "wgrt_scene_reserve", "wgrt_rays_init", "wgrt_scene_classify",
             "wgrt_locator_classify_host", "wgrt_selftest_math", "wgrt_status_string", "wgrt_last_error",
-            "wgrt_abi_version")
+            "wgrt_abi_version", "wgrt_eyebox_payload_floats", "wgrt_eyebox_pack", "wgrt_eyebox_assemble")
 EXPORTED_DEBUG = ("wgrt_debug_shadow", "wgrt_debug_scene_copy")
 
 
@@ -173,6 +173,12 @@ def load():
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
     L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
+    L.wgrt_eyebox_payload_floats.restype = ctypes.c_int64
+    L.wgrt_eyebox_payload_floats.argtypes = [ctypes.c_int64]
+    L.wgrt_eyebox_pack.restype = st
+    L.wgrt_eyebox_pack.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp]
+    L.wgrt_eyebox_assemble.restype = st
+    L.wgrt_eyebox_assemble.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp]
     # test / profiling hooks (include/wgrt_debug.h)
     L.wgrt_debug_shadow.restype = st
     L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,

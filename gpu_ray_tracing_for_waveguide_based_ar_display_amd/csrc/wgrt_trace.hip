@@ -680,6 +680,54 @@ __global__ __launch_bounds__(256) void rays_init_kernel(RayInitArgs A) {
     }
 }
 
+// Eyebox collection of the strong-scaling gather (include/wgrt.h wgrt_eyebox_*): row copies of whole
+// 80 x 120 slabs as 16-B loads / stores, one workgroup per (row, 1/kEbSlabParts of the slab).  The
+// spill rows (121 floats) move as dwords.
+constexpr int kEbSlabF4 = WGRT_EB_SLAB / 4;   // 2400 float4 per slab
+constexpr int kEbSlabParts = 3;               // 800 float4 per workgroup: 256 threads x 3-4
+
+__host__ __device__ inline int64_t eb_spill_floats(int64_t nb) { return (nb * WGRT_EB_SPILL + 3) / 4 * 4; }
+
+__global__ __launch_bounds__(256) void eyebox_pack_kernel(const float *eb, int64_t n_slabs, const int64_t *slabs,
+                                                          const int64_t *next, const float *mask, int64_t n, int64_t nb,
+                                                          float *payload) {
+    const int64_t j = blockIdx.y;
+    if (j >= n) return;
+    const int64_t s = slabs[j];
+    if (s < 0 || s >= n_slabs) return;
+    const float4 *src = (const float4 *)(eb + s * WGRT_EB_SLAB);
+    float4 *out = (float4 *)(payload + j * WGRT_EB_SLAB);
+    const int lo = (int)blockIdx.x * (kEbSlabF4 / kEbSlabParts), hi = lo + kEbSlabF4 / kEbSlabParts;
+    for (int c = lo + threadIdx.x; c < hi; c += blockDim.x) out[c] = src[c];
+    if (blockIdx.x == 0 && threadIdx.x < WGRT_EB_SPILL) {
+        const int64_t t = next[j];
+        const float v = (t >= 0 && t < n_slabs) ? eb[t * WGRT_EB_SLAB + threadIdx.x] * mask[j] : 0.0f;
+        payload[nb * WGRT_EB_SLAB + j * WGRT_EB_SPILL + threadIdx.x] = v;
+    }
+}
+
+__global__ __launch_bounds__(256) void eyebox_copy_kernel(float *eb, int64_t n_slabs, const float *recv, int64_t nb,
+                                                          int64_t plen, const int64_t *dst) {
+    const int64_t row = blockIdx.y;   // r * nb + j
+    const int64_t s = dst[row];
+    if (s < 0 || s >= n_slabs) return;
+    const int64_t r = row / nb, j = row % nb;
+    const float4 *src = (const float4 *)(recv + r * plen + j * WGRT_EB_SLAB);
+    float4 *out = (float4 *)(eb + s * WGRT_EB_SLAB);
+    const int lo = (int)blockIdx.x * (kEbSlabF4 / kEbSlabParts), hi = lo + kEbSlabF4 / kEbSlabParts;
+    for (int c = lo + threadIdx.x; c < hi; c += blockDim.x) out[c] = src[c];
+}
+
+__global__ __launch_bounds__(128) void eyebox_spill_kernel(float *eb, int64_t n_slabs, const float *recv, int64_t nb,
+                                                           int64_t plen, const int64_t *spill_dst) {
+    const int64_t row = blockIdx.x;
+    const int64_t s = spill_dst[row];
+    if (s < 0 || s >= n_slabs || threadIdx.x >= WGRT_EB_SPILL) return;
+    const int64_t r = row / nb, j = row % nb;
+    // one spill row per target slab (slab s's spill comes only from slab s - 1): no atomics needed
+    eb[s * WGRT_EB_SLAB + threadIdx.x] += recv[r * plen + nb * WGRT_EB_SLAB + j * WGRT_EB_SPILL + threadIdx.x];
+}
+
 __global__ __launch_bounds__(256) void selftest_math_kernel(const double *a, const double *b, int64_t n,
                                                             double *out) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1447,6 +1495,45 @@ wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t n
     DEVICE_SCOPE(dev_scope, sdev);
     const int64_t blocks = std::min<int64_t>((A.n + 255) / 256, 65536);
     hipLaunchKernelGGL(rays_init_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, A);
+    HIP_TRY(hipGetLastError());
+    return WGRT_OK;
+}
+
+int64_t wgrt_eyebox_payload_floats(int64_t nb) { return nb < 0 ? -1 : nb * WGRT_EB_SLAB + eb_spill_floats(nb); }
+
+wgrt_status wgrt_eyebox_pack(const float *eb, int64_t n_slabs, const int64_t *slabs, const int64_t *next,
+                             const float *spill_mask, int64_t n, int64_t nb, float *payload, void *stream) {
+    if (n < 0 || nb < n || n_slabs < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "need 0 <= n <= nb and n_slabs >= 0");
+    if (n == 0) return WGRT_OK;
+    if (!eb || !slabs || !next || !spill_mask || !payload) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (((uintptr_t)eb | (uintptr_t)payload) & 15) return fail(WGRT_ERR_INVALID_ARGUMENT, "eb / payload must be 16-B aligned");
+    if (n > 65535) return fail(WGRT_ERR_INVALID_ARGUMENT, "at most 65535 slabs per rank");
+    int sdev = 0;
+    HIP_TRY(stream_device(stream, &sdev));
+    DEVICE_SCOPE(dev_scope, sdev);
+    hipLaunchKernelGGL(eyebox_pack_kernel, dim3(kEbSlabParts, (unsigned)n), dim3(256), 0, (hipStream_t)stream, eb,
+                       n_slabs, slabs, next, spill_mask, n, nb, payload);
+    HIP_TRY(hipGetLastError());
+    return WGRT_OK;
+}
+
+wgrt_status wgrt_eyebox_assemble(float *eb, int64_t n_slabs, const float *recv, int32_t world, int64_t nb,
+                                 const int64_t *dst, const int64_t *spill_dst, void *stream) {
+    if (world < 0 || nb < 0 || n_slabs < 0) return fail(WGRT_ERR_INVALID_ARGUMENT, "negative world / nb / n_slabs");
+    const int64_t rows = (int64_t)world * nb;
+    if (rows == 0) return WGRT_OK;
+    if (!eb || !recv || !dst || !spill_dst) return fail(WGRT_ERR_INVALID_ARGUMENT, "NULL argument");
+    if (((uintptr_t)eb | (uintptr_t)recv) & 15) return fail(WGRT_ERR_INVALID_ARGUMENT, "eb / recv must be 16-B aligned");
+    if (rows > 65535) return fail(WGRT_ERR_INVALID_ARGUMENT, "at most 65535 payload rows");
+    int sdev = 0;
+    HIP_TRY(stream_device(stream, &sdev));
+    DEVICE_SCOPE(dev_scope, sdev);
+    const int64_t plen = wgrt_eyebox_payload_floats(nb);
+    hipLaunchKernelGGL(eyebox_copy_kernel, dim3(kEbSlabParts, (unsigned)rows), dim3(256), 0, (hipStream_t)stream, eb,
+                       n_slabs, recv, nb, plen, dst);
+    HIP_TRY(hipGetLastError());
+    hipLaunchKernelGGL(eyebox_spill_kernel, dim3((unsigned)rows), dim3(128), 0, (hipStream_t)stream, eb, n_slabs, recv,
+                       nb, plen, spill_dst);
     HIP_TRY(hipGetLastError());
     return WGRT_OK;
 }

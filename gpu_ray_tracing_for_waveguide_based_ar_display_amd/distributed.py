@@ -221,19 +221,22 @@ class EyeboxGather:
 
     ``all_blocks[r]``: global block ids of rank r (every rank knows the whole assignment, so
     the message sizes and placements need no exchange).  A rank's payload is one flat buffer,
-    ``[nb x 9600 slab floats | nb x SPILL spill floats]``, padded to the largest shard (the
-    collective needs equal sizes).  The send buffer and rank 0's receive buffers are allocated once
-    (first call per device and dtype) and reused; pack and assembly are device-side gathers and
-    scatters with every index precomputed on the host here, so a call makes no host round trip
-    before the collective.  The assembly writes each owned slab once, from the rank that traced it
-    (one ``index_copy_`` per rank), zeroes only slabs no rank owns, and adds the spills."""
+    ``[nb x 9600 slab floats | nb x SPILL spill floats, padded to 4]`` (include/wgrt.h
+    wgrt_eyebox_*), padded to the largest shard (the collective needs equal sizes).  The send buffer
+    and rank 0's receive buffer are allocated once (first call per device and dtype) and reused;
+    every index is precomputed on the host here, so a call makes no host round trip before the
+    collective.  On a HIP device the pack and the assembly are the library's row-copy kernels
+    (``wgrt_eyebox_pack`` / ``wgrt_eyebox_assemble``: one launch each, 16-B loads and stores, each
+    owned slab written once from the rank that traced it); host tensors (the gloo CPU tests) take the
+    same steps as torch gathers and scatters.  Slabs no rank owns are zeroed, spills added last."""
 
     def __init__(self, all_blocks, num_fov_x: int, num_fov_y: int, lambdas, n_lambda_scene: int, device=None):
         import torch
         self.n_slabs = n_lambda_scene * num_fov_y * num_fov_x
         self.world = len(all_blocks)
         self.nb = max(len(b) for b in all_blocks)
-        self.payload_len = self.nb * (EB_SLAB + SPILL)
+        self.spill_len = (self.nb * SPILL + 3) // 4 * 4
+        self.payload_len = self.nb * EB_SLAB + self.spill_len
         self.device = device
         t = lambda a, dt=torch.int64: torch.as_tensor(np.asarray(a), dtype=dt, device=device)
         self.slabs, self.nxt, self.spill_mask, self.spill_rows, self.spill_dst = [], [], [], [], []
@@ -256,6 +259,16 @@ class EyeboxGather:
             self.has_spill.append(bool(sp.any()))
         self.unowned = t(np.nonzero(~owned)[0])
         self.any_unowned = bool((~owned).any())
+        # the assembly's row maps (wgrt_eyebox_assemble): payload row j of rank r -> its slab and the slab
+        # its spill row adds to, -1 for padding rows and rows without a spill to move
+        dst = np.full((self.world, self.nb), -1, dtype=np.int64)
+        sdst = np.full((self.world, self.nb), -1, dtype=np.int64)
+        for r, b in enumerate(all_blocks):
+            sl = slab_ids(b, num_fov_x, num_fov_y, lambdas)
+            dst[r, :len(sl)] = sl
+            sp = self.spill_mask[r].cpu().numpy() > 0
+            sdst[r, :len(sl)][sp] = sl[sp] + 1
+        self.dst_rows, self.spill_dst_rows = t(dst.reshape(-1)), t(sdst.reshape(-1))
         self._bufs = {}
 
     def buffers(self, device, dtype, dst: bool):
@@ -271,7 +284,11 @@ class EyeboxGather:
 
     def _views(self, buf):
         nb = self.nb
-        return buf[:nb * EB_SLAB].view(nb, EB_SLAB), buf[nb * EB_SLAB:].view(nb, SPILL)
+        return buf[:nb * EB_SLAB].view(nb, EB_SLAB), buf[nb * EB_SLAB:nb * EB_SLAB + nb * SPILL].view(nb, SPILL)
+
+    @staticmethod
+    def _hip(t) -> bool:
+        return getattr(t, "is_cuda", False) and t.dtype.is_floating_point and t.element_size() == 4
 
     def pack(self, eb, rank: int, out=None):
         """Rank ``rank``'s payload, into ``out`` (the collective passes its reused send buffer) or a new
@@ -279,8 +296,15 @@ class EyeboxGather:
         import torch
         flat = eb.reshape(self.n_slabs, EB_SLAB)
         buf = out if out is not None else torch.zeros(self.payload_len, dtype=eb.dtype, device=eb.device)
-        main, spill = self._views(buf)
         n = self.counts[rank]
+        if self._hip(eb) and eb.is_contiguous():
+            from ._lib import check, load
+            from .engine import _stream_handle
+            check(load().wgrt_eyebox_pack(eb.data_ptr(), self.n_slabs, self.slabs[rank].data_ptr(),
+                                          self.nxt[rank].data_ptr(), self.spill_mask[rank].data_ptr(), n, self.nb,
+                                          buf.data_ptr(), _stream_handle(eb.device)), "wgrt_eyebox_pack")
+            return buf
+        main, spill = self._views(buf)
         torch.index_select(flat, 0, self.slabs[rank], out=main[:n])
         if self.has_spill[rank]:
             torch.index_select(flat[:, :SPILL], 0, self.nxt[rank], out=spill[:n])
@@ -289,10 +313,22 @@ class EyeboxGather:
 
     def assemble(self, eb, parts) -> None:
         """Rank 0: rebuild the whole grid in ``eb`` from every rank's payload (``parts[r]``: rank r's
-        flat payload, e.g. row r of the receive buffer)."""
+        flat payload; on a HIP device ``parts`` may be the [world, payload] receive buffer itself)."""
         flat = eb.reshape(self.n_slabs, EB_SLAB)
         if self.any_unowned:
             flat.index_fill_(0, self.unowned, 0)
+        recv = parts if hasattr(parts, "shape") else None
+        if self._hip(eb) and eb.is_contiguous():
+            import torch
+            if recv is None or not recv.is_contiguous():
+                recv = torch.stack(list(parts)) if not hasattr(parts, "shape") else parts.contiguous()
+            from ._lib import check, load
+            from .engine import _stream_handle
+            check(load().wgrt_eyebox_assemble(eb.data_ptr(), self.n_slabs, recv.data_ptr(), self.world, self.nb,
+                                              self.dst_rows.data_ptr(), self.spill_dst_rows.data_ptr(),
+                                              _stream_handle(eb.device)), "wgrt_eyebox_assemble")
+            return
+        parts = [recv[r] for r in range(self.world)] if recv is not None else parts
         for r, p in enumerate(parts):
             n = self.counts[r]
             if n:
@@ -318,7 +354,10 @@ class EyeboxGather:
             parts = [recv[r] for r in range(self.world)] if rank == dst else None
         dist.gather(payload, gather_list=parts, dst=dst, group=group)
         if rank == dst:
-            self.assemble(eb, [p.to(eb.device) for p in parts] if on_gloo_dev else parts)
+            if on_gloo_dev:
+                for r in range(self.world):
+                    recv[r].copy_(parts[r])
+            self.assemble(eb, recv)
         return eb
 
 

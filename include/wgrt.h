@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 5
+#define WGRT_ABI_VERSION 6
 
 typedef enum {
     WGRT_OK = 0,
@@ -259,6 +259,29 @@ wgrt_status wgrt_scene_reserve(const wgrt_scene *scene, int64_t n_rays, int num_
 wgrt_status wgrt_rays_init(const double *points, int64_t rays_per_fov, int32_t nx, int32_t ny,
                            const int32_t *lambdas, int32_t n_lambdas, int64_t block_lo, int64_t block_hi,
                            const wgrt_ray_columns *out, uint32_t *rng_states, void *stream);
+
+/* Multi-GPU eyebox collection (the strong-scaling gather of distributed.EyeboxGather; the reference
+ * runs one GPU and accumulates matrix_EB in place, MAIN:167-178).  Each rank traces its own FoV x
+ * wavelength blocks, so it owns whole (lambda, n, m) slabs of 80 x 120 floats of matrix_EB, plus -- by
+ * the compiled-numba aliasing of an out-coupling exactly on the eyebox's top edge (GRTF:154-165) -- the
+ * first WGRT_EB_SPILL floats of the slab after an owned one.  A rank's payload is one flat float
+ * buffer of wgrt_eyebox_payload_floats(nb) floats: nb slab rows of WGRT_EB_SLAB floats, then nb spill
+ * rows of WGRT_EB_SPILL floats (16-B aligned: the spill part is padded to 4 floats).
+ *   pack:     row j (j < n) <- slab slabs[j]; spill row j <- the first WGRT_EB_SPILL floats of slab
+ *             next[j], times spill_mask[j] (0 or 1); rows n .. nb-1 untouched.
+ *   assemble: eb slab dst[r * nb + j] <- slab row j of rank r's payload (recv + r * payload floats),
+ *             for every dst >= 0; then the spill rows with spill_dst[r * nb + j] >= 0 are ADDED to the
+ *             first WGRT_EB_SPILL floats of that slab (after every copy).  Slabs no dst names are left
+ *             as they are.
+ * Every pointer is DEVICE memory (slabs / next / dst / spill_dst int64, spill_mask float); both
+ * launch on `stream` (its device) and are asynchronous.  Not part of the reference. */
+#define WGRT_EB_SLAB 9600
+#define WGRT_EB_SPILL 121
+int64_t wgrt_eyebox_payload_floats(int64_t nb);
+wgrt_status wgrt_eyebox_pack(const float *eb, int64_t n_slabs, const int64_t *slabs, const int64_t *next,
+                             const float *spill_mask, int64_t n, int64_t nb, float *payload, void *stream);
+wgrt_status wgrt_eyebox_assemble(float *eb, int64_t n_slabs, const float *recv, int32_t world, int64_t nb,
+                                 const int64_t *dst, const int64_t *spill_dst, void *stream);
 
 /* Polygon membership of n points (DEVICE xy[n, 2]) through the scene's locator:
  * bit k of out_mask[i] = is_inside_or_on_edge(point i, polygon k) with polygon order
