@@ -191,7 +191,7 @@ def load():
     L.wgrt_last_error.argtypes = []
     L.wgrt_abi_version.restype = ctypes.c_int
     if L.wgrt_abi_version() not in _accept_abi:
-        raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} != expected {ABI_VERSION}")
+        raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} not in the accepted {_accept_abi}")
     _lib = L
     return L
 
