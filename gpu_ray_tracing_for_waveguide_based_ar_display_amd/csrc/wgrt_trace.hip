@@ -99,6 +99,7 @@ constexpr int kEpilogueGroups = 256;
 #endif
 constexpr int kQBlock = WGRT_QBLOCK;    // out-coupling queue slots a wave reserves at a time (a C3 wave
                                // out-couples ~10 rays per trace)
+static_assert(kQBlock >= 1 && kQBlock <= 64, "a queue block is binned by one lane per entry");
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     __shared__ unsigned long long red[4][5];
@@ -392,9 +393,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         if (om != 0ull) {
             const int nout = __popcll(om), rem = kQBlock - qfill;
             const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(om >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)om, 0));
+            // the entries past the current block take ceil(extra / kQBlock) new consecutive blocks, all
+            // but the last of them filled by this pass (a wave can out-couple more rays at once than a
+            // block holds)
+            const int extra = nout - rem;
+            const int nblk = extra > 0 ? (extra + kQBlock - 1) / kQBlock : 0;
             unsigned long long nb = 0;
-            if (nout > rem) {
-                if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)kQBlock);
+            if (nblk) {
+                if (lane == 0) nb = atomicAdd(KA(q_count), (unsigned long long)nblk * kQBlock);
                 nb = uni64(__shfl(nb, 0));
             }
             if (out) {   // entry: out-coupling position and the ray's (lambda, m, n) tile index
@@ -402,11 +408,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 KA(q_xy)[j] = double2{L.r.x, L.r.y};
                 KA(q_i)[j] = L.tix;
             }
-            if (nout > rem) {
-                // the old block is full: the epilogue bins it
-                if (qblk && lane == 0) KA(full_list)[atomicAdd(KA(full_count), 1ull)] = (uint32_t)(qbase / kQBlock);
-                qbase = nb;
-                qfill = nout - rem;
+            if (nblk) {
+                // the filled blocks -- the old one, and every new one but the last -- go to the epilogue
+                const uint32_t b0 = (uint32_t)(nb / kQBlock), old = (uint32_t)(qbase / kQBlock);
+                const int nfull = (qblk ? 1 : 0) + nblk - 1;
+                if (lane < nfull)
+                    KA(full_list)[atomicAdd(KA(full_count), 1ull)] = qblk ? (lane == 0 ? old : b0 + lane - 1) : b0 + lane;
+                qbase = nb + (unsigned long long)(nblk - 1) * kQBlock;
+                qfill = extra - (nblk - 1) * kQBlock;
                 qblk = true;
             } else {
                 qfill += nout;

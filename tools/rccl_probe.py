@@ -6,10 +6,10 @@ path with every rank on its own device.  This probe runs what that path asks of 
 RCCL communicator (``init_process_group("nccl", device_id=...)``, as bench.py does for N > 1), with
 the exact buffers, dtypes and call shapes of ``distributed.EyeboxGather`` and ``timed_run``:
 
-* the eyebox gather of an 8-rank C3 split: every virtual rank r's payload is packed on the device
-  (``wgrt_eyebox_pack``) from a traced grid and moved into rank 0's receive row r by ``dist.gather``
-  (one-rank gather: ``gather_list=[recv[r]]``); ``wgrt_eyebox_assemble`` then rebuilds the grid,
-  which must equal the traced one bit for bit;
+* the eyebox gather of an 8-rank C3 split: virtual rank r traces its interleaved shard into a grid
+  of its own, its payload is packed on the device (``wgrt_eyebox_pack``) and moved into rank 0's
+  receive row r by ``dist.gather`` (one-rank gather: ``gather_list=[recv[r]]``);
+  ``wgrt_eyebox_assemble`` then builds the grid, which must equal the whole batch's trace bit for bit;
 * ``dist.reduce`` (SUM, float32) of the grid -- the ``weak`` record's and ``--collective reduce``'s
   collective -- and the two small ``all_reduce``s of ``timed_run`` (MAX float64, SUM int64);
 * ``dist.barrier`` with the device bound at init.
@@ -42,32 +42,42 @@ def main():
     assert dist.get_backend() == "nccl" and dist.get_world_size() == 1
     rec = {"backend": dist.get_backend(), "torch": torch.__version__}
 
-    # one trace of the C3 batch: the grid the 8-way split would gather, with real hits and spills
+    # the C3 batch traced whole (the reference), and split 8 ways as the strong-scaling ranks trace it:
+    # virtual rank r traces its interleaved shard into its own grid (its slabs plus their spills)
     w = CONFIGS["C3"]
     nx, ny, lambdas, R = w.nx, w.ny, list(w.lambdas), w.R
     geom, luts, points = build_inputs(w)
     scene = Scene.from_geometry(geom, luts, device=0)
-    world = 8
-    blocks = [make_shard(nx, ny, len(lambdas), R, world, r).blocks for r in range(world)]
-    full = make_shard(nx, ny, len(lambdas), R, 1, 0)
-    rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(full)
+    build = hip_shard_builder(points, nx, ny, lambdas, R, dev)
+
+    def trace(shard, eb, st):
+        rays, rng = build(shard)
+        gm = shard.gid
+        kw = dict(gid_offset=gm.offset) if gm.offset is not None else dict(
+            gid_blocks=torch.as_tensor(gm.block_gid, device=dev), gid_block_rays=R)
+        trace_fullcolor(scene, rays, rng, eb, stats=st, **kw)
+
     eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
     st = new_stats(dev)
-    gm = full.gid
-    kw = dict(gid_offset=gm.offset) if gm.offset is not None else dict(
-        gid_blocks=torch.as_tensor(gm.block_gid, device=dev), gid_block_rays=R)
-    trace_fullcolor(scene, rays, rng, eb, stats=st, **kw)
+    trace(make_shard(nx, ny, len(lambdas), R, 1, 0), eb, st)
+    world = 8
+    shards = [make_shard(nx, ny, len(lambdas), R, world, r) for r in range(world)]
+    grids, st_r = [], new_stats(dev)
+    for sh in shards:
+        grids.append(torch.zeros_like(eb))
+        trace(sh, grids[-1], st_r)
     torch.cuda.synchronize()
     hits = int(st[2].item())
     assert hits > 0 and float(eb.sum().item()) == float(hits), "traced grid does not hold the hits"
+    assert int(st_r[2].item()) == hits and int(st_r[0].item()) == int(st[0].item()), "shards differ from the batch"
 
-    g = EyeboxGather(blocks, nx, ny, lambdas, scene.num_lmd, device=dev)
+    g = EyeboxGather([sh.blocks for sh in shards], nx, ny, lambdas, scene.num_lmd, device=dev)
     send, recv = g.buffers(dev, eb.dtype, True)
     recv.fill_(float("nan"))
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for r in range(world):
-        payload = g.pack(eb, r, out=send)
+        payload = g.pack(grids[r], r, out=send)
         dist.gather(payload, gather_list=[recv[r]], dst=0)
     out = torch.full_like(eb, float("nan"))
     g.assemble(out, recv)
@@ -76,8 +86,10 @@ def main():
     rec["payload_bytes_per_rank"] = int(g.payload_len * 4)
     if not torch.equal(out, eb):
         bad = int((out != eb).sum().item())
-        raise SystemExit(f"RCCL gather + assembly differs from the traced grid in {bad} cells")
+        raise SystemExit(f"RCCL gather + assembly of the 8 shards' grids differs from the batch's grid in {bad} cells")
     rec["gather_equal"] = True
+    spill = sum(int(g.has_spill[r]) for r in range(world))
+    rec["ranks_with_spill_rows"] = spill
 
     red = eb.clone()
     dist.reduce(red, dst=0, op=dist.ReduceOp.SUM)
@@ -90,7 +102,7 @@ def main():
     if not (torch.equal(red, eb) and float(t.item()) == 1.25 and int(b.item()) == int(st[0].item())):
         raise SystemExit("one-rank reduce / all_reduce changed their operands")
     rec.update(reduce_equal=True, all_reduce_ok=True, hits=hits, bounces=int(st[0].item()),
-               slabs_per_rank=[len(x) for x in blocks][:2])
+               slabs_per_rank=[len(sh.blocks) for sh in shards][:2])
     dist.destroy_process_group()
     scene.close()
     print(json.dumps(rec), flush=True)
