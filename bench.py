@@ -314,7 +314,7 @@ def main(argv=None):
                         "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
                     "binding": binding,
                     "note": "achieved = algorithmic bytes (72 B x bounces) / launch_avg_ms; launch_avg_ms: HIP events "
-                            "around each launch (trace kernel + its eyebox/replay epilogue kernel) on rank 0, in a "
+                            "around each launch (trace kernel + the kernel behind it: replay_kernel, or epilogue_kernel for fused calls) on rank 0, in a "
                             "second pass of the same K launches (the timed steps carry no event records); valu: the "
                             "issue-side bound SURVEY.md §8(d) calls binding (VALU busy = SQ_ACTIVE_INST_VALU x 4 / "
                             "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}

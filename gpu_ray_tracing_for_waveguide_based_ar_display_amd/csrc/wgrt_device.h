@@ -64,8 +64,11 @@ struct TraceArgs {
     int n_trace_waves;                  // partial slots of the trace kernel (one per workgroup)
     unsigned long long *heads0;         // this launch's counter set (kScratchCtr words)
     unsigned long long *other_ctr;      // the next launch's counter set, zeroed by this launch's epilogue
-    uint32_t *full_list;                // out-coupling queue blocks the trace waves filled (block numbers)
+    uint32_t *full_list;                // out-coupling queue blocks the trace waves filled (block numbers); with the
+                                        // in-kernel epilogue: per block, the link to the block its wave filled before
     unsigned long long *full_count;
+    unsigned long long *epi_acc;        // in-kernel epilogue: {bounces, bad_rays, eyebox_hits, interactions} totals ...
+    unsigned long long *epi_done;       // ... and the count of trace workgroups that have added theirs
     unsigned long long *timeline;       // debug: per-wave timeline (wgrt_debug_opts), timeline kernels only
     int64_t timeline_waves;
     // fused launches (variants 7 / 9, n_iter > 1): n_iter chained traces of every ray in one

@@ -81,9 +81,24 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 // count and the out-coupling queue count, each on its own 128-B line.
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
-constexpr int kScratchCtr = (kHeads + 3) * kHeadStride;   // heads, replay / queue / full-block counts
+constexpr int kScratchCtr = (kHeads + 5) * kHeadStride;   // heads, replay / queue / full-block counts, epilogue totals / done
 
-// Runs right behind every Jones-vector launch on its stream -- the launch's only other kernel:
+// Single launches do their epilogue in the trace kernel (fused launches keep epilogue_kernel, whose
+// replays chain the traces after an abandoned one): every wave bins the out-coupling blocks it filled
+// when it ends (a chain of block links, its own stores), every workgroup adds its counter totals with
+// agent-scope atomics and counts itself done, and the workgroup that counts last adds the totals to
+// *stats and zeroes the next launch's counter set.  Abandoned rays are re-traced by replay_kernel
+// behind the launch, which reads one count and leaves when there are none.  A replay call inside the
+// trace kernel (a non-inlined trace_one) gave the wave loop 128 VGPRs and 536 B of scratch per lane and
+// lost 14-27 %; this design gains 1-4 % on single launches.  WGRT_INKERNEL_EPI=0
+// builds the epilogue-kernel design for single launches too.
+#ifndef WGRT_INKERNEL_EPI
+#define WGRT_INKERNEL_EPI 1
+#endif
+constexpr bool kInKernelEpilogue = WGRT_INKERNEL_EPI != 0;
+
+// Runs right behind every fused Jones-vector launch on its stream (and every single launch built with
+// WGRT_INKERNEL_EPI=0) -- the launch's only other kernel:
 //  1. bins the out-coupling queue blocks the trace waves filled (a wave bins the block it holds
 //     when it leaves; cells count hits, +1.0f, so the binning order does not matter);
 //  2. re-traces the rays the launch abandoned (uncertain decisions; nothing of them was written)
@@ -232,6 +247,7 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
 template <bool FUSED, bool SINGLE, bool TL, class Loc>
 __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, const Loc &loc, unsigned long long *heads,
                                           int chunk) {
+    constexpr bool EPI = !FUSED && kInKernelEpilogue;
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
@@ -328,7 +344,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         entry = true;
     };
     // a trace's counters are added when it ends: an abandoned trace (kUncertain) adds nothing, and its
-    // replay (epilogue_kernel, trace_one) counts the whole trace once
+    // replay (replay_kernel or, fused, epilogue_kernel: trace_one) counts the whole trace once
     auto retire = [&]() {
         tot_b += L.bounces;
         tot_int += L.inter;
@@ -376,8 +392,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 out = true;
                 retire();
             } else if (next == kUncertain) {
-                // abandoned with no side effect; replay_kernel re-traces it (fused: from this
-                // iteration on, so later iterations skip the ray)
+                // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel, from
+                // this iteration on, so later iterations skip the ray)
                 if (FUSED)
                     __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
                                        __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -409,11 +425,18 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 KA(q_i)[j] = L.tix;
             }
             if (nblk) {
-                // the filled blocks -- the old one, and every new one but the last -- go to the epilogue
                 const uint32_t b0 = (uint32_t)(nb / kQBlock), old = (uint32_t)(qbase / kQBlock);
-                const int nfull = (qblk ? 1 : 0) + nblk - 1;
-                if (lane < nfull)
-                    KA(full_list)[atomicAdd(KA(full_count), 1ull)] = qblk ? (lane == 0 ? old : b0 + lane - 1) : b0 + lane;
+                if (EPI) {
+                    // new block k links to the block this wave filled before it (+1; 0: none): the wave
+                    // walks the chain back when it ends and bins every block it filled
+                    if (lane < nblk) KA(full_list)[b0 + lane] = lane > 0 ? b0 + lane : (qblk ? old + 1u : 0u);
+                } else {
+                    // the filled blocks -- the old one, and every new one but the last -- go to the epilogue
+                    const int nfull = (qblk ? 1 : 0) + nblk - 1;
+                    if (lane < nfull)
+                        KA(full_list)[atomicAdd(KA(full_count), 1ull)] =
+                            qblk ? (lane == 0 ? old : b0 + lane - 1) : b0 + lane;
+                }
                 qbase = nb + (unsigned long long)(nblk - 1) * kQBlock;
                 qfill = extra - (nblk - 1) * kQBlock;
                 qblk = true;
@@ -561,17 +584,28 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one
     // lane per entry, its own stores read back (agent-scope loads, past the L1)
     uint32_t tot_h = 0;
+    auto bin = [&](unsigned long long j) {
+        const uint32_t g = __hip_atomic_load(KA(q_i) + j, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double *pq = (const double *)(KA(q_xy) + j);
+        const double px = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const double py = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const int ny = KA(ny), nx = KA(nx);
+        const int en = (int)(g % (uint32_t)ny), em = (int)(g / (uint32_t)ny % (uint32_t)nx);
+        const int el = (int)(g / ((uint32_t)ny * (uint32_t)nx));
+        tot_h += eyebox_add(A, el, em, en, px, py) ? 1u : 0u;
+    };
     if (qblk) {
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        if (lane < qfill) {
-            const uint32_t g = __hip_atomic_load(KA(q_i) + qbase + lane, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double *pq = (const double *)(KA(q_xy) + qbase + lane);
-            const double px = __hip_atomic_load(pq, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const double py = __hip_atomic_load(pq + 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            const int ny = KA(ny), nx = KA(nx);
-            const int en = (int)(g % (uint32_t)ny), em = (int)(g / (uint32_t)ny % (uint32_t)nx);
-            const int el = (int)(g / ((uint32_t)ny * (uint32_t)nx));
-            tot_h = eyebox_add(A, el, em, en, px, py) ? 1u : 0u;
+        if (lane < qfill) bin(qbase + lane);
+        if (EPI) {   // ... and, with the in-kernel epilogue, every block it filled before, along the links
+            uint32_t prev = __builtin_amdgcn_readfirstlane(
+                __hip_atomic_load(KA(full_list) + qbase / kQBlock, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            while (prev != 0u) {
+                const uint32_t b = prev - 1u;
+                if (lane < kQBlock) bin((unsigned long long)b * kQBlock + lane);
+                prev = __builtin_amdgcn_readfirstlane(
+                    __hip_atomic_load(KA(full_list) + b, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT));
+            }
         }
     }
     if (TL && tl_on && lane == 0) {
@@ -594,15 +628,66 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         red[threadIdx.x >> 6][3] = sum_g;
         red[threadIdx.x >> 6][4] = sum_i;
     }
+    if (!EPI) {
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            unsigned long long *slot = KA(part) + kPartWords * (size_t)blockIdx.x;
+            slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+            slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+            slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+            slot[3] = red[0][3] + red[1][3] + red[2][3] + red[3][3];
+            slot[4] = red[0][4] + red[1][4] + red[2][4] + red[3][4];
+        }
+        return;
+    }
+    // In-kernel epilogue: one lane adds the workgroup's totals with agent-scope atomics, waits for
+    // them, and counts the workgroup done; the workgroup that counts last reads the totals at agent
+    // scope, adds them to *stats and zeroes the next launch's counter set (every other workgroup has
+    // left this one's)
+    __shared__ int last_wg;
     __syncthreads();
     if (threadIdx.x == 0) {
-        unsigned long long *slot = KA(part) + kPartWords * (size_t)blockIdx.x;
-        slot[0] = red[0][0] + red[1][0] + red[2][0] + red[3][0];
-        slot[1] = red[0][1] + red[1][1] + red[2][1] + red[3][1];
-        slot[2] = red[0][2] + red[1][2] + red[2][2] + red[3][2];
-        slot[3] = red[0][3] + red[1][3] + red[2][3] + red[3][3];
-        slot[4] = red[0][4] + red[1][4] + red[2][4] + red[3][4];
+        unsigned long long *const acc = KA(epi_acc);
+        const unsigned long long t_b = red[0][0] + red[1][0] + red[2][0] + red[3][0];
+        const unsigned long long t_bad = red[0][1] + red[1][1] + red[2][1] + red[3][1];
+        const unsigned long long t_h = red[0][2] + red[1][2] + red[2][2] + red[3][2];
+        const unsigned long long t_i = red[0][4] + red[1][4] + red[2][4] + red[3][4];
+        if (t_b) atomicAdd(acc + 0, t_b);
+        if (t_bad) atomicAdd(acc + 1, t_bad);
+        if (t_h) atomicAdd(acc + 2, t_h);
+        if (t_i) atomicAdd(acc + 3, t_i);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        last_wg = atomicAdd(KA(epi_done), 1ull) == (unsigned long long)gridDim.x - 1ull;
     }
+    __syncthreads();
+    if (!last_wg) return;
+    unsigned long long *const oc = KA(other_ctr);
+    for (int k = threadIdx.x; k < kScratchCtr; k += blockDim.x) oc[k] = 0ull;
+    wgrt_trace_stats *const st = KA(stats);
+    if (threadIdx.x == 0 && st) {
+        unsigned long long *const acc = KA(epi_acc);
+        unsigned long long t[4];
+        for (int k = 0; k < 4; ++k) t[k] = __hip_atomic_load(acc + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        if (t[3]) atomicAdd((unsigned long long *)&st->interactions, t[3]);
+        if (t[0]) atomicAdd((unsigned long long *)&st->bounces, t[0]);
+        if (t[1]) atomicAdd((unsigned long long *)&st->bad_rays, t[1]);
+        if (t[2]) atomicAdd((unsigned long long *)&st->eyebox_hits, t[2]);
+    }
+}
+
+// The replay kernel behind a single launch with the in-kernel epilogue: re-traces the launch's
+// abandoned rays from their launch-start state with the reference arithmetic, one per thread (usually
+// there are none: every workgroup reads one count and leaves).
+constexpr int kReplayGroups = 64;
+__global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
+    const unsigned long long nr = *A.replay_count;
+    if (nr == 0ull) return;
+    uint64_t b = 0, h = 0, bad = 0, ni = 0;
+    for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr;
+         k += (unsigned long long)gridDim.x * blockDim.x)
+        trace_one(A, (int64_t)A.replay_list[k], b, h, bad, nullptr, &ni);
+    add_stats(A.stats, b, h, bad, ni);
+    if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats) atomicAdd((unsigned long long *)&A.stats->replayed, nr);
 }
 
 // Variants 7 / 9: the persistent loop over the Jones-vector path (32-bit cell words; 64-bit
@@ -1342,6 +1427,8 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.q_count = ctr + (kHeads + 1) * kHeadStride;
     A.full_count = ctr + (kHeads + 2) * kHeadStride;
     A.full_list = sc->full;
+    A.epi_acc = ctr + (kHeads + 3) * kHeadStride;
+    A.epi_done = ctr + (kHeads + 4) * kHeadStride;
     A.heads0 = ctr;
     A.other_ctr = sc->ctr + (size_t)(parity ^ 1u) * kScratchCtr;
     A.part = sc->part;
@@ -1380,7 +1467,11 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         return fail(WGRT_ERR_HIP, "fault injection: failed after the trace kernel (wgrt_debug_opts.fail_after_trace)");
     }
     if (e == hipSuccess) {
-        hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
+        // fused launches keep the epilogue kernel (their replays chain the traces after the abandoned one)
+        if (num_iter > 1 || !kInKernelEpilogue)
+            hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
+        else
+            hipLaunchKernelGGL(replay_kernel, dim3(kReplayGroups), dim3(256), 0, st, A);
         e = hipGetLastError();
     }
     if (e != hipSuccess) {
