@@ -72,7 +72,9 @@ constexpr int kJHeader = 16;
 // rare double-precision re-evaluation), the bounds W[k] and cosA_2 in double.
 constexpr int kJBlock = 48;       // line 0: cosA[2], f32 {Wsum, cosA_2}, herm32[3][4]; rec[3][8], W[3], cosA_2
 constexpr int kJBlockCos = 0;     // cosA_0, cosA_1
-constexpr int kJBlockF32 = 2;     // floats: Wsum (sum of W[k], rounded up), cosA_2, 0, 0
+constexpr int kJBlockF32 = 2;     // floats: Wsum (sum of W[k], rounded up), cosA_2, the tile's kJGrowth (rounded up), 0;
+                                  // block 0 (two branches, the in-coupling event): Wsum, kJGrowth (rounded up), and
+                                  // the bits of the double kJCosIc1 in the last two
 constexpr int kJBlockHerm = 4;    // floats [3][4]: h11, h22, Re h12, Im h12
 constexpr int kJBlockRec = 16;    // the three matrices in double precision
 constexpr int kJBlockCos2 = 43;   // cosA_2 in double

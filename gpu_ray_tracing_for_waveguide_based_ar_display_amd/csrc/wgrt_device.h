@@ -815,9 +815,14 @@ __device__ __forceinline__ void jones_decide(JDecision &d, double u, double scl,
 // A block's {cosA_0, cosA_1, cosA_2, Wsum} for the estimate: cosA_0 and cosA_1 in double (the
 // taken branch's efficiency uses them), cosA_2 and Wsum from their floats (the exact cosA_2 is
 // read only by the rare double-precision re-evaluation, estimate64).
-__device__ __forceinline__ double4 block_cw(const double *B) {
+// The same loads also bring what the tile header would otherwise be loaded for: the phase-growth bound,
+// and for block 0 (entry: the in-coupling event) the event's denominator cos(ic1) (kJBlockF32; block 0's
+// cosA_2 slot holds the growth bound, and a two-branch block never reads cosA_2).
+__device__ __forceinline__ double4 block_cw(const double *B, bool entry, double &growth, double &cos_ic1) {
     const double2 c01 = *(const double2 *)(B + kJBlockCos);
     const float4 fw = *(const float4 *)(B + kJBlockF32);
+    growth = (double)(entry ? fw.y : fw.z);
+    cos_ic1 = __hiloint2double(__float_as_int(fw.w), __float_as_int(fw.z));
     return double4{c01.x, c01.y, (double)fw.y, (double)fw.x};
 }
 
@@ -879,19 +884,19 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     // 1134, 1147, ...); each is also the miss hop of the region it leads to (R5 never hops)
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    const double2 cg = *(const double2 *)(T + kJCosIc1);          // cos(ic1 angle), phase growth
-    const double4 cw = block_cw(B);
+    double growth, cos_ic1;
+    const double4 cw = block_cw(B, entry, growth, cos_ic1);
     // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
     // issued together with its matrix, one memory round trip per interaction less
     const double2 mva = *(const double2 *)(T + kJGap + ga);
     const double2 mvb = *(const double2 *)(T + kJGap + gb);
-    const double denom = entry ? cg.x : r.cos_t;
+    const double denom = entry ? cos_ic1 : r.cos_t;
     const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
     const double inv = rcp_nr(denom);
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double base = fma(nb * nb, cg.y, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double base = fma(nb * nb, growth, 1.0) * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);

@@ -211,9 +211,18 @@ WGRT_HD void pack_tile(const PackView &v, int64_t g, double *T, double *J) {
             h[3] = (float)((pr * ri - pi * rr) + (qr * si - qi * sr));   // Im(conj(p) r + conj(q) s)
         }
         f32[0] = (float)(sum * 1.01);   // 1.01: covers this bound's own rounding to float
-        f32[1] = (float)Bt[kBlockCos + 2];
-        f32[2] = 0.0f;
-        f32[3] = 0.0f;
+        // the phase-growth bound with the block's line-0 loads (it only ever scales a tolerance up, so
+        // rounded up); block 0 also carries the in-coupling event's denominator cos(ic1) as the bits
+        // of a double, in place of the cosA_2 it does not have
+        const float growth = (float)(J[kJGrowth] * 1.000001);
+        if (b == 0) {
+            f32[1] = growth;
+            O[kJBlockF32 + 1] = J[kJCosIc1];
+        } else {
+            f32[1] = (float)Bt[kBlockCos + 2];
+            f32[2] = growth;
+            f32[3] = 0.0f;
+        }
     }
 }
 

@@ -151,13 +151,14 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
                 jr.mi = fma(mr, hp.y, jr.mi * hp.x);
             }
             hops = 0;
-            const double4 cw = block_cw(JB);
-            const double jden = entry ? J[kJCosIc1] : cos_th;
+            double growth, cos_ic1;
+            const double4 cw = block_cw(JB, entry, growth, cos_ic1);
+            const double jden = entry ? cos_ic1 : cos_th;
             const double inv = rcp_nr(jden);
             const double f01 = entry ? A.n_g : 1.0;
             const double nb = (double)bounces * 0.01;
             const double en2 = fma(jr.er, jr.er, fma(jr.ei, jr.ei, fma(jr.mr, jr.mr, jr.mi * jr.mi)));
-            const double base = fma(nb * nb, J[kJGrowth], 1.0) * fabs(inv) * fmax(en2, 1.0);
+            const double base = fma(nb * nb, growth, 1.0) * fabs(inv) * fmax(en2, 1.0);
             const double c_ref[3] = {e0, e0 + e1, e0 + e1 + e2};
             // how much of each bound the arithmetic uses against the reference's thresholds
             auto ratio = [&](const JDecision &d, double scl) {
