@@ -1019,7 +1019,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
     const bool die = over | !eff1 | (!ic & !hit & (region == 5));           // GRTF:1244-1246
     const bool sw = !die & !ic & !hit & (region == 3) & !eff2;              // GRTF:1103-1104: R3 -> R4, no move
     const bool hop = !die & !ic & !hit & !sw;                               // miss hop
-    const int blkbase = fc ? 3 + (region - 2) * nfc : 3 + 2 * nfc + (region - 4) * noc;
+    // the region's first block: FC regions 2-3 follow the 3 in-coupler states, OC regions 4-5 both FC
+    // regions (one multiply of selected operands: no divergent branch)
+    const int blkbase = 3 + (fc ? 0 : 2 * nfc) + (region - (fc ? 2 : 4)) * count;
     L.bounces += over ? 0u : 1u;
     kind = ic ? 0 : region - 1;
     r.region = sw ? 4 : region;
@@ -1035,7 +1037,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
         r.mi = fma(mr, r.hi, r.mi * r.hr);
         L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
-    return die ? kDie : ic ? 1 + region : hit ? blkbase + sl : kTransit;
+    const int step = hit ? blkbase + sl : kTransit;
+    const int next = ic ? 1 + region : step;
+    return die ? kDie : next;
 }
 
 template <class LaneT>

@@ -194,7 +194,11 @@ constexpr int kFusedRefill = 16;
 #ifndef WGRT_STRIPE
 #define WGRT_STRIPE 16
 #endif
-constexpr int64_t kStripe = WGRT_STRIPE;   // chunks per stripe of the work queue (1024 rays: one C3 tile)
+constexpr int64_t kStripe = WGRT_STRIPE;
+#ifndef WGRT_ONE_RETIRE
+#define WGRT_ONE_RETIRE 1
+#endif
+constexpr bool kOneRetire = WGRT_ONE_RETIRE != 0;   // one retire site per pass (single launches)   // chunks per stripe of the work queue (1024 rays: one C3 tile)
 
 // How long a fused-launch lane may wait for its ray's previous trace before it gives the trace
 // up (wgrt_trace_stats.handoff_giveups; the Python layer raises on it).  A legitimate wait for
@@ -248,6 +252,11 @@ template <bool FUSED, bool SINGLE, bool TL, class Loc>
 __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, const Loc &loc, unsigned long long *heads,
                                           int chunk) {
     constexpr bool EPI = !FUSED && kInKernelEpilogue;
+    // single launches retire a finished trace at one place per pass, right after advance(): the rays
+    // that ended in the previous pass's interaction and those advance() ends (fused launches retire at
+    // once: their hand-off would wait a pass)
+    constexpr bool ONE = !FUSED && kOneRetire;
+    bool fin = false;
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
@@ -390,7 +399,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
             const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry);
             if (next == kOut) {
                 out = true;
-                retire();
+                if (ONE) {
+                    fin = true;
+                    active = false;
+                } else {
+                    retire();
+                }
             } else if (next == kUncertain) {
                 // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel, from
                 // this iteration on, so later iterations skip the ray)
@@ -400,7 +414,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
                 active = false;
             } else if (next < 0) {
-                retire();
+                if (ONE) {
+                    fin = true;
+                    active = false;
+                } else {
+                    retire();
+                }
             } else {
                 L.r.region = next;
             }
@@ -450,7 +469,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         if (active) {
             blk = advance(A, K, loc, L, kind);
             entry = false;
-            if (blk == kDie) retire();
+            if (ONE) fin |= blk == kDie;
+            else if (blk == kDie) retire();
+        }
+        if (ONE && fin) {   // before the refill, which reuses the lane
+            retire();
+            fin = false;
         }
         if (FUSED && waiting) {
             // poll only the previous trace's granule: the ray's columns are still in L from the
@@ -575,7 +599,12 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
             if (!first && active) {
                 blk = advance(A, K, loc, L, kind);
                 entry = false;
-                if (blk == kDie) retire();
+                if (ONE) fin |= blk == kDie;
+                else if (blk == kDie) retire();
+            }
+            if (ONE && fin) {
+                retire();
+                fin = false;
             }
             if (__ballot(active) == 0ull) break;
             interact_pass();
