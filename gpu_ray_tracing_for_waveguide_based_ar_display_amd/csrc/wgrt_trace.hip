@@ -397,14 +397,17 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         if (active && blk >= 0) {
             L.inter += entry ? 0u : 1u;
             const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry);
-            if (next == kOut) {
+            if (ONE) {
+                // straight-line: a trace that ended (out-coupled or died) is retired at the next
+                // pass's retire site; an abandoned one (rare) goes to the replay list
+                out = next == kOut;
+                fin = (next < 0) & (next != kUncertain);
+                active = next >= 0;
+                L.r.region = next >= 0 ? next : L.r.region;
+                if (next == kUncertain) KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+            } else if (next == kOut) {
                 out = true;
-                if (ONE) {
-                    fin = true;
-                    active = false;
-                } else {
-                    retire();
-                }
+                retire();
             } else if (next == kUncertain) {
                 // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel, from
                 // this iteration on, so later iterations skip the ray)
@@ -414,12 +417,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
                 active = false;
             } else if (next < 0) {
-                if (ONE) {
-                    fin = true;
-                    active = false;
-                } else {
-                    retire();
-                }
+                retire();
             } else {
                 L.r.region = next;
             }
