@@ -184,7 +184,7 @@ WGRT_HD bool inside_or_on_edge_subset(double px, double py, const double *xy, in
 template <class GidFn>
 WGRT_HD double rng_draw_lazy(uint32_t &s, GidFn gid) {
     uint32_t v = s;
-    if (v == 0u) v = 0x6D2B79F5u ^ (uint32_t)(gid() + 1);
+    if (__builtin_expect(v == 0u, 0)) v = 0x6D2B79F5u ^ (uint32_t)(gid() + 1);
     v ^= v << 13;
     v ^= v >> 17;
     v ^= v << 5;

@@ -900,7 +900,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
-    if (!d.ok) {   // rare: the double-precision evaluation
+    if (__builtin_expect(!d.ok, 0)) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
         jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     }
@@ -1004,7 +1004,7 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
     const bool e1edge = ((c >> (2 * kPolyEff1)) & 3u) == 2u;
     const bool sedge = region >= 2 && cand != 0 && !((in >> low_bit((W)(cand | kTop))) & 1u);
     const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
-    if (e1edge | sedge | e2edge) {
+    if (__builtin_expect(e1edge | sedge | e2edge, 0)) {
         c = resolve_edges(K, loc, c, region, first, count, r.x, r.y);
         f = (c >> (2 * first)) & gmask;
         in = f & kLow;

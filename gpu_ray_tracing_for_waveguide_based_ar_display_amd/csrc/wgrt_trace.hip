@@ -357,7 +357,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     auto retire = [&]() {
         tot_b += L.bounces;
         tot_int += L.inter;
-        if (tot_b >= 0x80000000u) {
+        if (__builtin_expect(tot_b >= 0x80000000u, 0)) {
             wgrt_trace_stats *const st = KA(stats);
             if (st) atomicAdd((unsigned long long *)&st->bounces, (unsigned long long)tot_b);
             tot_b = 0;
@@ -404,7 +404,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 fin = (next < 0) & (next != kUncertain);
                 active = next >= 0;
                 L.r.region = next >= 0 ? next : L.r.region;
-                if (next == kUncertain) KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+                if (__builtin_expect(next == kUncertain, 0))
+                    KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
             } else if (next == kOut) {
                 out = true;
                 retire();
