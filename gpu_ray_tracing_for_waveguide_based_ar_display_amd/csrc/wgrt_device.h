@@ -184,7 +184,7 @@ __device__ __forceinline__ Cell locate(const Loc &L, double x, double y) {
 template <class Loc>
 __device__ __forceinline__ bool in_poly(const Loc &L, const Cell &c, int k, double x, double y) {
     const unsigned cls = (unsigned)(c.w >> (2 * k)) & 3u;
-    if (cls != 2u) return cls == 1u;
+    if (__builtin_expect(cls != 2u, 1)) return cls == 1u;   // IN / OUT; EDGE cells are rare (0.34 % of C3 lane-passes)
     const int a = L.poly_off[k], nv = L.poly_off[k + 1] - a;
     const int r = k * L.ncy + c.cy;
     const int e0 = L.row_off[r], e1 = L.row_off[r + 1];
@@ -233,7 +233,7 @@ __device__ __forceinline__
 #endif
 bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y, const KArgs *Kp = nullptr) {
     const unsigned cls = (unsigned)(w >> (2 * k)) & 3u;
-    if (cls != 2u) return cls == 1u;
+    if (__builtin_expect(cls != 2u, 1)) return cls == 1u;   // IN / OUT; EDGE cells are rare (0.34 % of C3 lane-passes)
     const int cy = (int)floor((y - L.y0) * L.inv_h);   // an EDGE cell is inside the grid
     const int r = k * L.ncy + cy;
     const bool KARG = Kp != nullptr;
@@ -242,7 +242,7 @@ bool in_poly_w(const Loc &L, typename Loc::Word w, int k, double x, double y, co
     const double *const bands = KARG ? KLOCP(Kp, bands) : L.bands;
     const double4 *rec = (const double4 *)(bands + (size_t)r * 4 * kBandSegs);
     const double4 s0 = rec[0], s1 = rec[1], s2 = rec[2], s3 = rec[3];
-    if (s0.x != INFINITY) {
+    if (__builtin_expect(s0.x != INFINITY, 1)) {   // else: a row with more edges than a band record holds
         bool inside = false;
         const double4 sg[kBandSegs] = {s0, s1, s2, s3};
 #pragma unroll

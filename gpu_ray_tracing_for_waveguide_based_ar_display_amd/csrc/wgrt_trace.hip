@@ -329,7 +329,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                                          (FUSED && L.k > 0) ? KA(rng64) + L.i : nullptr, &w);
         waiting = false;
         active = false;
-        if (!ok) {
+        if (__builtin_expect(!ok, 0)) {
             ++tot_bad;
             return;
         }
