@@ -261,7 +261,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
     const int64_t n_iter = FUSED ? A.n_iter : 1;
     int head = xcc_id();
-    int64_t cur = 0, end = 0;         // rays of the current item still to hand out (wave-uniform)
+    // rays of the current item still to hand out (wave-uniform; 32-bit: variants 7 / 9 index < 2^32 rays,
+    // so the refill's compares stay scalar)
+    uint32_t cur = 0, end = 0;
     // debug timeline (TL instantiations only): per wave, start / queue exhausted / end
     // (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD, and the passes /
     // lane-passes up to the queue running dry
@@ -544,28 +546,28 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 }
                 const int32_t *const ord = KA(order);
                 const int64_t cc = (!FUSED && ord) ? (int64_t)ord[c] : c;
-                cur = cc * chunk;
+                cur = (uint32_t)(cc * chunk);
                 const int64_t nr = KA(n_rays);
-                end = cur + chunk < nr ? cur + chunk : nr;
+                end = (uint32_t)((int64_t)cur + chunk < nr ? (int64_t)cur + chunk : nr);
                 cur_k = k;
                 sb ^= 1;
                 sbase_prev = sbase;
-                sbase = (uint32_t)cur;
+                sbase = cur;
                 ++staged;
-                if (lane < (int)(end - cur)) stage_chunk(K, sbufs + sb * (kStageCols * 64), cur + lane);
+                if (lane < (int)(end - cur)) stage_chunk(K, sbufs + sb * (kStageCols * 64), (int64_t)cur + lane);
             }
             const int want = __popcll(need);
-            const int64_t avail = end - cur;
-            const int take = (int64_t)want < avail ? want : (int)avail;
+            const uint32_t avail = end - cur;
+            const int take = (uint32_t)want < avail ? want : (int)avail;
             if ((need >> lane) & 1ull) {
                 const int rank = __builtin_amdgcn_mbcnt_hi((uint32_t)(need >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)need, 0));
                 if (rank < take) {
-                    L.i = cur + rank;
+                    L.i = cur + (uint32_t)rank;
                     L.k = cur_k;
                     taken = true;
                 }
             }
-            cur += take;
+            cur += (uint32_t)take;
             need = __ballot(!active && !waiting && !taken);
         }
         // the rays taken from every item of this refill start together: one round trip for
@@ -574,7 +576,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
             // lane j prepares slot j of the new chunk; the LDS stores precede the refilled lanes'
             // reads of other lanes' slots in the wave's (in-order) LDS queue
-            if (lane < (int)(end - (int64_t)sbase)) prep_staged(A, K, sbufs + sb * (kStageCols * 64), lane);
+            if (lane < (int)(end - sbase)) prep_staged(A, K, sbufs + sb * (kStageCols * 64), lane);
             asm volatile("" ::: "memory");
         }
         if (taken) {
