@@ -78,7 +78,8 @@ __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
 }
 
 // Launch scratch counters of the Jones-vector variants: kHeads work-queue heads, then the replay
-// count and the out-coupling queue count, each on its own 128-B line.
+// count, the out-coupling queue and full-block counts, and a single launch's epilogue totals and done
+// count, each on its own 128-B line.
 constexpr int kHeadStride = 16;   // unsigned long longs between heads (128 B)
 constexpr int kHeads = 8;
 constexpr int kScratchCtr = (kHeads + 5) * kHeadStride;   // heads, replay / queue / full-block counts, epilogue totals / done
@@ -644,7 +645,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         tl[8 * tl_wave + 4] = tl_lanes;
         tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
     }
-    // the workgroup's counters go to its partial slot (summed by the epilogue: no contended atomics)
+    // the workgroup's counters: a fused launch's go to its partial slot (summed by epilogue_kernel), a
+    // single launch's to the epilogue totals below (one atomic each per workgroup: not contended)
     __shared__ unsigned long long red[4][5];
     const uint64_t sum_b = wave_sum((uint64_t)tot_b);
     const uint64_t sum_bad = wave_sum((uint64_t)tot_bad);
