@@ -103,6 +103,25 @@ def test_interaction_counts_with_replays(dev, oracle_runs, name, num_iter):
     np.testing.assert_array_equal(got[0]["rng"], want[num_iter - 1]["rng"])
     assert int(st[0]) == sum(want[k]["total"] for k in range(num_iter))
     assert int(st[5]) == sum(want[k]["inter"] for k in range(num_iter)), (int(st[5]), [w["inter"] for w in want])
+    np.testing.assert_array_equal(got[0]["eb"], want[num_iter - 1]["eb"])
+    if num_iter == 1:
+        np.testing.assert_array_equal(got[0]["bounces"], want[0]["bounces"])
+
+
+def test_every_ray_replayed(dev, oracle_runs):
+    """Bounds so wide that no decision is certified: every traced ray is abandoned at its in-coupling
+    event and re-traced by the kernel behind the launch (replay_kernel for a single launch: more rays
+    than its threads, so its grid-stride loop runs).  Results, counters and per-ray bounces equal the
+    oracle's."""
+    c, want = oracle_runs("C2")
+    got = _run(c, dev, 7, debug=dict(cert_tol=1e3, cert_tol32=1e3))
+    st = got[0]["stats"]
+    traced = c.N - int(st[1])
+    assert int(st[3]) == traced > 64 * 256
+    np.testing.assert_array_equal(got[0]["rng"], want[0]["rng"])
+    np.testing.assert_array_equal(got[0]["eb"], want[0]["eb"])
+    np.testing.assert_array_equal(got[0]["bounces"], want[0]["bounces"])
+    assert int(st[0]) == want[0]["total"] and int(st[5]) == want[0]["inter"]
 
 
 @pytest.mark.parametrize("k", [-1.0, 2.0, 40.0])
