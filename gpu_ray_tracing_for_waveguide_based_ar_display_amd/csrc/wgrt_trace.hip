@@ -409,21 +409,22 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 L.r.region = next >= 0 ? next : L.r.region;
                 if (__builtin_expect(next == kUncertain, 0))
                     KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
-            } else if (next == kOut) {
-                out = true;
-                retire();
-            } else if (next == kUncertain) {
-                // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel, from
-                // this iteration on, so later iterations skip the ray)
-                if (FUSED)
-                    __hip_atomic_store(KA(rng64) + L.i, ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
-                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
-                active = false;
-            } else if (next < 0) {
-                retire();
             } else {
-                L.r.region = next;
+                // one retire site for both ends of a trace (out-coupled, died)
+                out = next == kOut;
+                L.r.region = next >= 0 ? next : L.r.region;
+                if (__builtin_expect(next == kUncertain, 0)) {
+                    // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel,
+                    // from this iteration on, so later iterations skip the ray)
+                    if (FUSED)
+                        __hip_atomic_store(KA(rng64) + L.i,
+                                           ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                    KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+                    active = false;
+                } else if (next < 0) {
+                    retire();
+                }
             }
         }
         const uint64_t om = __ballot(out);
