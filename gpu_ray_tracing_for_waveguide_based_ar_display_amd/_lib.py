@@ -139,6 +139,12 @@ def load():
         L = ctypes.CDLL(path, mode=ctypes.RTLD_GLOBAL)
     except OSError as e:
         raise WgrtError(f"cannot load {path}: {e}") from e
+    # the ABI first: an accepted earlier build (tools only, use_library) may lack later entry points
+    L.wgrt_abi_version.restype = ctypes.c_int
+    L.wgrt_abi_version.argtypes = []
+    abi = L.wgrt_abi_version()
+    if abi not in _accept_abi:
+        raise WgrtError(f"libwgrt ABI {abi} not in the accepted {_accept_abi}")
     st = ctypes.c_int
     L.wgrt_scene_create.restype = st
     L.wgrt_scene_create.argtypes = [ctypes.POINTER(SceneDesc), ctypes.c_int, ctypes.POINTER(_vp)]
@@ -173,12 +179,13 @@ def load():
     L.wgrt_selftest_math.argtypes = [_vp, _vp, ctypes.c_int64, _vp, _vp]
     L.wgrt_scene_reserve.restype = st
     L.wgrt_scene_reserve.argtypes = [_vp, ctypes.c_int64, ctypes.c_int, _vp]
-    L.wgrt_eyebox_payload_floats.restype = ctypes.c_int64
-    L.wgrt_eyebox_payload_floats.argtypes = [ctypes.c_int64]
-    L.wgrt_eyebox_pack.restype = st
-    L.wgrt_eyebox_pack.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp]
-    L.wgrt_eyebox_assemble.restype = st
-    L.wgrt_eyebox_assemble.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp]
+    if abi >= 6:   # the strong-scaling gather's row-copy kernels (ABI 6)
+        L.wgrt_eyebox_payload_floats.restype = ctypes.c_int64
+        L.wgrt_eyebox_payload_floats.argtypes = [ctypes.c_int64]
+        L.wgrt_eyebox_pack.restype = st
+        L.wgrt_eyebox_pack.argtypes = [_vp, ctypes.c_int64, _vp, _vp, _vp, ctypes.c_int64, ctypes.c_int64, _vp, _vp]
+        L.wgrt_eyebox_assemble.restype = st
+        L.wgrt_eyebox_assemble.argtypes = [_vp, ctypes.c_int64, _vp, ctypes.c_int32, ctypes.c_int64, _vp, _vp, _vp]
     # test / profiling hooks (include/wgrt_debug.h)
     L.wgrt_debug_shadow.restype = st
     L.wgrt_debug_shadow.argtypes = [_vp, ctypes.POINTER(Rays), ctypes.c_int64, ctypes.c_int64, ctypes.c_int, _vp,
@@ -189,9 +196,6 @@ def load():
     L.wgrt_status_string.argtypes = [ctypes.c_int]
     L.wgrt_last_error.restype = ctypes.c_char_p
     L.wgrt_last_error.argtypes = []
-    L.wgrt_abi_version.restype = ctypes.c_int
-    if L.wgrt_abi_version() not in _accept_abi:
-        raise WgrtError(f"libwgrt ABI {L.wgrt_abi_version()} not in the accepted {_accept_abi}")
     _lib = L
     return L
 

@@ -716,6 +716,43 @@ struct JField {
     double er, ei, mr, mi;
 };
 
+// Diagnostic segment stamps of a launch-tail pass (tools/segments.py).  Only a build with
+// -DWGRT_SEG (an experimental library, never the product) executes any of this: s_memtime at fixed
+// points of the pass, each segment's shader cycles summed per wave in scalar registers, and forced
+// vmcnt(0) waits at the ends of the two load segments, which separate a load's wait from the arithmetic
+// that overlaps it in the real kernel -- so the build's SHARES are read, not its length.
+// s[0] advance, s[1] retire / ballots, s[2] line-0 loads + the draw and bound arithmetic until they have
+// landed, s[3] estimate + decision, s[4] the taken branch's cell word, hop and matrix until landed,
+// s[5] field update, s[6] the rest of the pass (in-coupler test, outcome, out-coupling queue), s[7] passes.
+struct SegAcc {
+    uint32_t s[8];   // 32-bit sums of 32-bit differences (a tail is < 2^32 cycles): 9 SGPRs, not 18
+    uint32_t last;
+};
+#ifdef WGRT_SEG
+__device__ __forceinline__ uint32_t seg_stamp() {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t)::"memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return (uint32_t)t;
+}
+#define SEG_WAITVM(sg)                                        \
+    do {                                                      \
+        if (sg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
+    } while (0)
+#define SEG_MARK(sg, k)                                 \
+    do {                                                \
+        if (sg) {                                       \
+            const uint32_t t_ = seg_stamp();    \
+            (sg)->s[k] += t_ - (sg)->last;              \
+            (sg)->last = t_;                            \
+        }                                               \
+    } while (0)
+#else
+#define SEG_WAITVM(sg) ((void)0)
+#define SEG_MARK(sg, k) ((void)0)
+#endif
+
 struct Rec {
     double pr, pi, qr, qi, rr, ri, sr, si;
 };
@@ -829,9 +866,11 @@ __device__ __forceinline__ double4 block_cw(const double *B, bool entry, double 
 // The efficiencies from the single-precision Hermitian forms (the estimate every decision starts
 // with).  cw = {cosA_0, cosA_1, cosA_2, Wsum}.
 __device__ __forceinline__ void estimate32(JDecision &d, const double *B, const JRay &r, bool three, double inv,
-                                           double f01, double inv_n_g, const double4 &cw) {
+                                           double f01, double inv_n_g, const double4 &cw, SegAcc *sg = nullptr) {
     const float4 *H = (const float4 *)(B + kJBlockHerm);
     const float4 h0 = H[0], h1 = H[1];
+    SEG_WAITVM(sg);   // (the third branch's form is loaded after the mark: its wait counts in s[3])
+    SEG_MARK(sg, 2);
     const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
     const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
     const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
@@ -873,7 +912,7 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // are the same values the all-double evaluation gives.
 template <bool SINGLE, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
-                                        int kind, bool entry) {
+                                        int kind, bool entry, SegAcc *sg = nullptr) {
     JRay &r = L.r;
     const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
@@ -898,12 +937,13 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
     const double base = fma(nb * nb, growth, 1.0) * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
-    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw);
+    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     if (__builtin_expect(!d.ok, 0)) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
         jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     }
+    SEG_MARK(sg, 3);
     // one exit for every outcome but a taken branch; an out-coupling is appended to the
     // out-coupling queue by the caller (at (r.x, r.y))
     const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
@@ -921,7 +961,14 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
     // in-coupler states and R5 never hop), loaded with the taken branch's matrix
     const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
+#ifdef WGRT_SEG
+    const Rec rec_b = load_rec(B + kJBlockRec + 8 * b);
+    SEG_WAITVM(sg);
+    SEG_MARK(sg, 4);
+    const JField f = jones(rec_b, r);
+#else
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
+#endif
     // Ete = Ete1 / norm, Etm = Etm1 / norm (GRTF:874-876); the TIR step is in the TM row
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
@@ -940,6 +987,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     r.gy = mv.y;
     r.hr = hop.x;
     r.hi = hop.y;
+    SEG_MARK(sg, 5);
     if (kind == 0) {
         const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y, &K);
         if (ba) return in_ic ? 0 : 2;

@@ -237,6 +237,55 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
     return (epoch << 9) | (broken ? 0x100u : 0u) | k;
 }
 
+#ifndef WGRT_INKERNEL_REPLAY
+#define WGRT_INKERNEL_REPLAY 0
+#endif
+
+// An abandoned ray (kUncertain) onto the replay list.  With the in-kernel replay the entry is stored at
+// agent scope and waited for here, so it is in memory before this lane's workgroup counts itself done
+// (the last workgroup reads the list at agent scope); rare, so the wait costs nothing measurable.
+__device__ __forceinline__ void record_abandoned(const KArgs &K, uint32_t i) {
+    uint32_t *const slot = KA(replay_list) + atomicAdd(KA(replay_count), 1ull);
+#if WGRT_INKERNEL_REPLAY
+    __hip_atomic_store(slot, i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#else
+    *slot = i;
+#endif
+}
+
+#if WGRT_INKERNEL_REPLAY
+#ifdef WGRT_REPLAY_NOINLINE
+#define WGRT_REPLAY_INL __attribute__((noinline))
+#else
+#define WGRT_REPLAY_INL __forceinline__
+#endif
+// The single launch's replay inside the trace kernel (the last workgroup; wgrt_trace.hip jones_body): the
+// reference-arithmetic lane (trace_one) over the replay list, its TraceArgs read from the kernarg segment
+// here, so nothing of it is live across the wave loop.
+__device__ WGRT_REPLAY_INL void replay_tail(const KArgs &K, unsigned long long nr) {
+    TraceArgs R{};
+    R.x = KA(x); R.y = KA(y); R.m = KA(m); R.n = KA(n); R.l = KA(l);
+    R.te = KA(te); R.tm = KA(tm); R.dph = KA(dph);
+    R.rng = KA(rng); R.eb = KA(eb); R.stats = KA(stats); R.per_ray = KA(per_ray);
+    R.n_rays = KA(n_rays); R.gid_offset = KA(gid_offset);
+    R.gid_blocks = KA(gid_blocks); R.gid_block_rays = KA(gid_block_rays);
+    R.tiles = KA(tiles); R.tile_d = KA(tile_d);
+    R.nfc = KA(nfc); R.noc = KA(noc); R.nx = KA(nx); R.ny = KA(ny); R.nl = KA(nl);
+    R.n_g = KA(n_g); R.inv_n_g = KA(inv_n_g); R.threshold = KA(threshold);
+    R.loc.cells = KLOC(cells); R.loc.verts = KLOC(verts); R.loc.poly_off = KLOC(poly_off);
+    R.loc.row_off = KLOC(row_off); R.loc.row_edges = KLOC(row_edges); R.loc.bands = KLOC(bands);
+    R.loc.x0 = KLOC(x0); R.loc.y0 = KLOC(y0); R.loc.inv_h = KLOC(inv_h); R.loc.ncx = KLOC(ncx); R.loc.ncy = KLOC(ncy);
+    const uint32_t *const list = KA(replay_list);
+    uint64_t b = 0, h = 0, bad = 0, ni = 0;
+    for (unsigned long long k = threadIdx.x; k < nr; k += blockDim.x)
+        trace_one(R, (int64_t)__hip_atomic_load(list + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), b, h, bad,
+                  nullptr, &ni);
+    add_stats(R.stats, b, h, bad, ni);
+    if (threadIdx.x == 0 && R.stats) atomicAdd((unsigned long long *)&R.stats->replayed, nr);
+}
+#endif
+
 // The persistent loop of the Jones-vector variants.  Work items are 64-ray chunks handed out
 // by the per-XCD heads.  FUSED: a launch runs A.n_iter chained traces of every ray (the
 // reference's num_iter loop of launches, MAIN:169-177, each starting from the RNG state the
@@ -269,10 +318,15 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // (s_memrealtime, 100 MHz), passes, lane-passes with a ray in flight, XCD, and the passes /
     // lane-passes up to the queue running dry
     unsigned long long *const tl = TL ? KA(timeline) : nullptr;
+#ifdef WGRT_SEG
+    constexpr int kTlWords = 16;   // diagnostic segment build: 8 timeline words + 8 segment sums per wave
+#else
+    constexpr int kTlWords = 8;
+#endif
     const int64_t tl_wave = (int64_t)blockIdx.x * (blockDim.x >> 6) + (threadIdx.x >> 6);
-    const bool tl_on = TL && tl != nullptr && tl_wave < KA(timeline_waves);
+    const bool tl_on = TL && tl != nullptr && tl_wave < KA(timeline_waves) * 8 / kTlWords;
     unsigned long long tl_passes = 0, tl_lanes = 0;
-    if (tl_on && lane == 0) tl[8 * tl_wave] = __builtin_amdgcn_s_memrealtime();
+    if (tl_on && lane == 0) tl[kTlWords * tl_wave] = __builtin_amdgcn_s_memrealtime();
     uint32_t cur_k = 0;               // the item's iteration
     bool exhausted = false;
     bool active = false, waiting = false, taken = false;
@@ -391,7 +445,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // the second half of a pass: the interaction of the lanes at one, then this pass's
     // out-couplings into the wave's block of queue slots (a contended returning atomic per pass
     // would put its latency on every pass; a new block is needed about once per hundred passes)
-    auto interact_pass = [&]() {
+    auto interact_pass = [&](SegAcc *sg) {
         if (TL && tl_on) {
             ++tl_passes;
             tl_lanes += __popcll(__ballot(active));
@@ -399,7 +453,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         bool out = false;
         if (active && blk >= 0) {
             L.inter += entry ? 0u : 1u;
-            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry);
+            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
             if (ONE) {
                 // straight-line: a trace that ended (out-coupled or died) is retired at the next
                 // pass's retire site; an abandoned one (rare) goes to the replay list
@@ -407,8 +461,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 fin = (next < 0) & (next != kUncertain);
                 active = next >= 0;
                 L.r.region = next >= 0 ? next : L.r.region;
-                if (__builtin_expect(next == kUncertain, 0))
-                    KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+                if (__builtin_expect(next == kUncertain, 0)) record_abandoned(K, L.i);
             } else {
                 // one retire site for both ends of a trace (out-coupled, died)
                 out = next == kOut;
@@ -420,7 +473,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                         __hip_atomic_store(KA(rng64) + L.i,
                                            ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
                                            __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    KA(replay_list)[atomicAdd(KA(replay_count), 1ull)] = (uint32_t)L.i;
+                    record_abandoned(K, L.i);
                     active = false;
                 } else if (next < 0) {
                     retire();
@@ -466,6 +519,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 qfill += nout;
             }
         }
+        SEG_MARK(sg, 6);
     };
 
     for (;;) {
@@ -540,9 +594,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 if (!got) {
                     exhausted = true;
                     if (TL && tl_on && lane == 0) {
-                        tl[8 * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
-                        tl[8 * tl_wave + 6] = tl_passes;
-                        tl[8 * tl_wave + 7] = tl_lanes;
+                        tl[kTlWords * tl_wave + 1] = __builtin_amdgcn_s_memrealtime();
+                        tl[kTlWords * tl_wave + 6] = tl_passes;
+                        tl[kTlWords * tl_wave + 7] = tl_lanes;
                     }
                     break;
                 }
@@ -589,7 +643,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
         // the tail loop below
         if (!FUSED && exhausted) break;
-        interact_pass();
+        interact_pass(nullptr);
     }
     if (!FUSED && __ballot(active) != 0ull) {
         // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
@@ -598,20 +652,39 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // cell words before the decision here (one or two round trips less per interaction) lost
         // 1.5 % and 6 %: the chip is still full of rays when the queue runs dry.
         // The first pass continues the one the main loop broke off (advance and refill done).
+#ifdef WGRT_SEG
+        SegAcc seg{};
+        SegAcc *const sg = (TL && tl_on) ? &seg : nullptr;
+#else
+        SegAcc *const sg = nullptr;
+#endif
         for (bool first = true;; first = false) {
+#ifdef WGRT_SEG
+            if (sg) seg.last = seg_stamp();
+#endif
             if (!first && active) {
                 blk = advance(A, K, loc, L, kind);
                 entry = false;
                 if (ONE) fin |= blk == kDie;
                 else if (blk == kDie) retire();
             }
+            SEG_MARK(sg, 0);
             if (ONE && fin) {
                 retire();
                 fin = false;
             }
             if (__ballot(active) == 0ull) break;
-            interact_pass();
+            SEG_MARK(sg, 1);
+#ifdef WGRT_SEG
+            seg.s[7] += 1;
+#endif
+            interact_pass(sg);
         }
+#ifdef WGRT_SEG
+        // segment sums: words 8..15 of a 16-word wave record (tools/segments.py)
+        if (sg && lane == 0)
+            for (int k = 0; k < 8; ++k) tl[kTlWords * tl_wave + 8 + k] = seg.s[k];
+#endif
     }
     // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one
     // lane per entry, its own stores read back (agent-scope loads, past the L1)
@@ -641,10 +714,10 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         }
     }
     if (TL && tl_on && lane == 0) {
-        tl[8 * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
-        tl[8 * tl_wave + 3] = tl_passes;
-        tl[8 * tl_wave + 4] = tl_lanes;
-        tl[8 * tl_wave + 5] = (unsigned long long)xcc_id();
+        tl[kTlWords * tl_wave + 2] = __builtin_amdgcn_s_memrealtime();
+        tl[kTlWords * tl_wave + 3] = tl_passes;
+        tl[kTlWords * tl_wave + 4] = tl_lanes;
+        tl[kTlWords * tl_wave + 5] = (unsigned long long)xcc_id();
     }
     // the workgroup's counters: a fused launch's go to its partial slot (summed by epilogue_kernel), a
     // single launch's to the epilogue totals below (one atomic each per workgroup: not contended)
@@ -706,6 +779,13 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         if (t[1]) atomicAdd((unsigned long long *)&st->bad_rays, t[1]);
         if (t[2]) atomicAdd((unsigned long long *)&st->eyebox_hits, t[2]);
     }
+#if WGRT_INKERNEL_REPLAY
+    // the abandoned rays (none in practice): re-traced here, by the workgroup that counted last, with
+    // the reference arithmetic -- no replay kernel behind the launch.  Every list entry was stored at
+    // agent scope and waited for by its lane before that lane's workgroup counted itself done.
+    const unsigned long long nr = __hip_atomic_load(KA(replay_count), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (__builtin_expect(nr != 0ull, 0)) replay_tail(K, nr);
+#endif
 }
 
 // The replay kernel behind a single launch with the in-kernel epilogue: re-traces the launch's
@@ -1503,7 +1583,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         // fused launches keep the epilogue kernel (their replays chain the traces after the abandoned one)
         if (num_iter > 1 || !kInKernelEpilogue)
             hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
-        else
+        else if (!WGRT_INKERNEL_REPLAY || timeline)   // (the timeline kernels keep the replay kernel)
             hipLaunchKernelGGL(replay_kernel, dim3(kReplayGroups), dim3(256), 0, st, A);
         e = hipGetLastError();
     }

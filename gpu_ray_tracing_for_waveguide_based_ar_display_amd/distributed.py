@@ -270,6 +270,19 @@ class EyeboxGather:
             sdst[r, :len(sl)][sp] = sl[sp] + 1
         self.dst_rows, self.spill_dst_rows = t(dst.reshape(-1)), t(sdst.reshape(-1))
         self._bufs = {}
+        self._dev_idx = {}
+
+    def _idx(self, device):
+        """The index tensors on ``device`` (moved once per device and cached): the HIP kernels take their
+        raw pointers, so they must live on the grid's own device whatever ``device=`` the gather was
+        built with."""
+        key = str(device)
+        if key not in self._dev_idx:
+            mv = lambda v: v.to(device)
+            self._dev_idx[key] = dict(slabs=[mv(v) for v in self.slabs], nxt=[mv(v) for v in self.nxt],
+                                      spill_mask=[mv(v) for v in self.spill_mask], dst_rows=mv(self.dst_rows),
+                                      spill_dst_rows=mv(self.spill_dst_rows), unowned=mv(self.unowned))
+        return self._dev_idx[key]
 
     def buffers(self, device, dtype, dst: bool):
         """(send, recv): the payload buffer and, on the gathering rank, the [world, payload] receive
@@ -300,8 +313,11 @@ class EyeboxGather:
         if self._hip(eb) and eb.is_contiguous():
             from ._lib import check, load
             from .engine import _stream_handle
-            check(load().wgrt_eyebox_pack(eb.data_ptr(), self.n_slabs, self.slabs[rank].data_ptr(),
-                                          self.nxt[rank].data_ptr(), self.spill_mask[rank].data_ptr(), n, self.nb,
+            if buf.device != eb.device or not buf.is_contiguous() or buf.numel() < self.payload_len:
+                raise ValueError("EyeboxGather.pack: out must be a contiguous payload buffer on the grid's device")
+            ix = self._idx(eb.device)
+            check(load().wgrt_eyebox_pack(eb.data_ptr(), self.n_slabs, ix["slabs"][rank].data_ptr(),
+                                          ix["nxt"][rank].data_ptr(), ix["spill_mask"][rank].data_ptr(), n, self.nb,
                                           buf.data_ptr(), _stream_handle(eb.device)), "wgrt_eyebox_pack")
             return buf
         main, spill = self._views(buf)
@@ -315,17 +331,20 @@ class EyeboxGather:
         """Rank 0: rebuild the whole grid in ``eb`` from every rank's payload (``parts[r]``: rank r's
         flat payload; on a HIP device ``parts`` may be the [world, payload] receive buffer itself)."""
         flat = eb.reshape(self.n_slabs, EB_SLAB)
+        ix = self._idx(eb.device)
         if self.any_unowned:
-            flat.index_fill_(0, self.unowned, 0)
+            flat.index_fill_(0, ix["unowned"], 0)
         recv = parts if hasattr(parts, "shape") else None
         if self._hip(eb) and eb.is_contiguous():
             import torch
             if recv is None or not recv.is_contiguous():
                 recv = torch.stack(list(parts)) if not hasattr(parts, "shape") else parts.contiguous()
+            if recv.device != eb.device:
+                recv = recv.to(eb.device)
             from ._lib import check, load
             from .engine import _stream_handle
             check(load().wgrt_eyebox_assemble(eb.data_ptr(), self.n_slabs, recv.data_ptr(), self.world, self.nb,
-                                              self.dst_rows.data_ptr(), self.spill_dst_rows.data_ptr(),
+                                              ix["dst_rows"].data_ptr(), ix["spill_dst_rows"].data_ptr(),
                                               _stream_handle(eb.device)), "wgrt_eyebox_assemble")
             return
         parts = [recv[r] for r in range(self.world)] if recv is not None else parts
