@@ -17,7 +17,7 @@ PKG = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(PKG, "libwgrt.so")   # the in-tree build, the only one the product binds
 OPS_PATH = os.path.join(PKG, "_wgrt_torch.so")   # the torch operator library (csrc/wgrt_torch.cpp)
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 # include/wgrt.h (the drop-in boundary) and include/wgrt_debug.h (test / profiling hooks)
 EXPORTED = ("wgrt_scene_create", "wgrt_scene_create_ex", "wgrt_scene_destroy", "wgrt_scene_get_info",
             "wgrt_trace_fullcolor", "wgrt_trace_fullcolor_ex", "wgrt_trace_single", "wgrt_trace_single_ex",
@@ -62,7 +62,8 @@ class Rays(ctypes.Structure):
 class TraceStats(ctypes.Structure):
     _fields_ = [("bounces", ctypes.c_uint64), ("bad_rays", ctypes.c_uint64),
                 ("eyebox_hits", ctypes.c_uint64), ("replayed", ctypes.c_uint64),
-                ("handoff_giveups", ctypes.c_uint64), ("interactions", ctypes.c_uint64)]
+                ("handoff_giveups", ctypes.c_uint64), ("interactions", ctypes.c_uint64),
+                ("libm_rays", ctypes.c_uint64)]
 
 
 STATS_LEN = len(TraceStats._fields_)   # int64 words of a wgrt_trace_stats (torch stats tensors)

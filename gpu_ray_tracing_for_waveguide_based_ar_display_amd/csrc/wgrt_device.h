@@ -316,6 +316,7 @@ struct Lane {
     int l, m, n;
     uint32_t bounces;  // 1 in-coupling event + loop iterations (GRTF:905)
     bool hit;          // accumulated into matrix_EB
+    bool libm;         // a guard product ener * e_k fell below 2^-1000 (wgrt_trace_stats.libm_rays)
 };
 
 // Load ray i (GRTF:846-859).  Returns false (and leaves the lane empty) for a ray whose
@@ -340,6 +341,7 @@ __device__ __forceinline__ bool lane_load(const TraceArgs &A, int64_t i, Lane &L
     L.r.region = 0;
     L.bounces = 1;
     L.hit = false;
+    L.libm = false;
     return true;
 }
 
@@ -439,6 +441,14 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const Loc &loc, Lane
         }
         double e2 = 0.0;
         if (three) e2 = (te[2] * te[2] + tm[2] * tm[2]) * B[2] / denom / A.n_g;
+        // the ener-underflow regime: a guard product ener * e_k (GRTF:1020, 1073, 1136,
+        // ...) of a nonzero efficiency below 2^-1000, next to the subnormal range, where whether it rounds
+        // to zero -- and so the decision -- hangs on the last bits of the libm's cos / sin / atan2.  The
+        // certain path above never gets here with such a product (it needs ener > 1e-200 and every
+        // nonzero a_k > 1e-100), so checking this path sees every one.
+        if (thr)
+            L.libm |= ((e0 > 0.0) & (r.ener * e0 < 0x1p-1000)) | ((e1 > 0.0) & (r.ener * e1 < 0x1p-1000)) |
+                      (three & (e2 > 0.0) & (r.ener * e2 < 0x1p-1000));
         if (u <= e0 && (!thr || r.ener * e0 > t)) b = 0;
         else if (u <= e0 + e1 && (!thr || r.ener * e1 > t)) b = 1;
         else if (three && u <= e0 + e1 + e2 && r.ener * e2 > t) b = 2;
@@ -602,6 +612,7 @@ struct JRay {
     double eerr;             // relative error bound of ener (threshold > 0 kernels only)
     double gx, gy;           // miss-hop move of the current region
     double hr, hi;           // miss-hop phase step e^{2 i lut_TIR} of the current region, applied at each hop
+    float amp;               // bound on the amplification of the lanes' state discrepancy so far (>= 1; §2.4)
     uint32_t s;
     int region;
 };
@@ -701,6 +712,7 @@ __device__ __forceinline__ bool lane_load_staged(const LdsU32 *S, int j, int64_t
     L.r.cos_t = 1.0;
     L.r.ener = 1.0;
     L.r.eerr = 0.0;
+    L.r.amp = 1.0f;
     L.r.gx = L.r.gy = 0.0;
     L.r.hr = 1.0;
     L.r.hi = 0.0;
@@ -724,9 +736,11 @@ struct JField {
 // s[0] advance, s[1] retire / ballots, s[2] line-0 loads + the draw and bound arithmetic until they have
 // landed, s[3] estimate + decision, s[4] the taken branch's cell word, hop and matrix until landed,
 // s[5] field update, s[6] the rest of the pass (in-coupler test, outcome, out-coupling queue), s[7] passes.
+// The sums live in the wave's own LDS words (p[0..7], p[8] = the last stamp), updated by the wave's first
+// active lane: a mark inside exec-masked code then still adds to the wave's sums (register sums there
+// become per-lane vector values).  32-bit sums of 32-bit differences: a tail is < 2^32 cycles.
 struct SegAcc {
-    uint32_t s[8];   // 32-bit sums of 32-bit differences (a tail is < 2^32 cycles): 9 SGPRs, not 18
-    uint32_t last;
+    uint32_t __attribute__((address_space(3))) *p;
 };
 #ifdef WGRT_SEG
 __device__ __forceinline__ uint32_t seg_stamp() {
@@ -740,17 +754,45 @@ __device__ __forceinline__ uint32_t seg_stamp() {
     do {                                                      \
         if (sg) asm volatile("s_waitcnt vmcnt(0)" ::: "memory"); \
     } while (0)
-#define SEG_MARK(sg, k)                                 \
-    do {                                                \
-        if (sg) {                                       \
-            const uint32_t t_ = seg_stamp();    \
-            (sg)->s[k] += t_ - (sg)->last;              \
-            (sg)->last = t_;                            \
-        }                                               \
+// dep: a value the segment computes; the stamp takes it as an operand, so the compiler cannot sink
+// that arithmetic past the stamp (IR passes move arithmetic across an asm statement otherwise)
+__device__ __forceinline__ uint32_t seg_stamp_dep(double dep) {
+    unsigned long long t;
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t) : "v"(dep) : "memory");
+    __builtin_amdgcn_sched_barrier(0);
+    return (uint32_t)t;
+}
+__device__ __forceinline__ bool seg_first_lane() {
+    return (threadIdx.x & 63) == __builtin_amdgcn_readfirstlane(threadIdx.x & 63);
+}
+#define SEG_MARK_DEP(sg, k, dep)                              \
+    do {                                                      \
+        if (sg) {                                             \
+            const uint32_t t_ = seg_stamp_dep((double)(dep)); \
+            if (seg_first_lane()) {                           \
+                (sg)->p[k] += t_ - (sg)->p[8];                \
+                (sg)->p[8] = t_;                              \
+            }                                                 \
+        }                                                     \
     } while (0)
+#define SEG_MARK(sg, k) SEG_MARK_DEP(sg, k, 0.0)
+#if WGRT_SEG == 2
+// -DWGRT_SEG=2: wave-uniform marks only (the top level of a pass, jones_body); the interior marks below
+// sit in exec-masked code, whose stamps run only when a lane is there and whose sums the compiler merges
+// in vector registers
+#define SEG_IWAITVM(sg) ((void)0)
+#define SEG_IMARK_DEP(sg, k, dep) ((void)0)
 #else
+#define SEG_IWAITVM(sg) SEG_WAITVM(sg)
+#define SEG_IMARK_DEP(sg, k, dep) SEG_MARK_DEP(sg, k, dep)
+#endif
+#else
+#define SEG_IWAITVM(sg) ((void)0)
+#define SEG_IMARK_DEP(sg, k, dep) ((void)0)
 #define SEG_WAITVM(sg) ((void)0)
 #define SEG_MARK(sg, k) ((void)0)
+#define SEG_MARK_DEP(sg, k, dep) ((void)0)
 #endif
 
 struct Rec {
@@ -866,11 +908,16 @@ __device__ __forceinline__ double4 block_cw(const double *B, bool entry, double 
 // The efficiencies from the single-precision Hermitian forms (the estimate every decision starts
 // with).  cw = {cosA_0, cosA_1, cosA_2, Wsum}.
 __device__ __forceinline__ void estimate32(JDecision &d, const double *B, const JRay &r, bool three, double inv,
-                                           double f01, double inv_n_g, const double4 &cw, SegAcc *sg = nullptr) {
+                                           double f01, double inv_n_g, const double4 &cw, SegAcc *sg = nullptr,
+                                           float4 *h01 = nullptr) {
     const float4 *H = (const float4 *)(B + kJBlockHerm);
     const float4 h0 = H[0], h1 = H[1];
-    SEG_WAITVM(sg);   // (the third branch's form is loaded after the mark: its wait counts in s[3])
-    SEG_MARK(sg, 2);
+    if (h01) {
+        h01[0] = h0;
+        h01[1] = h1;
+    }
+    SEG_IWAITVM(sg);   // (the third branch's form is loaded after the mark: its wait counts in s[3])
+    SEG_IMARK_DEP(sg, 2, h0.x + h1.x);
     const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
     const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
     const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
@@ -943,7 +990,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
         jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     }
-    SEG_MARK(sg, 3);
+    SEG_IMARK_DEP(sg, 3, d.a0 + d.a1 + d.a2 + (d.ok ? 1.0 : 0.0) + (d.s0 ? 2.0 : 0.0) + (d.s1 ? 4.0 : 0.0));
     // one exit for every outcome but a taken branch; an out-coupling is appended to the
     // out-coupling queue by the caller (at (r.x, r.y))
     const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
@@ -963,8 +1010,8 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
 #ifdef WGRT_SEG
     const Rec rec_b = load_rec(B + kJBlockRec + 8 * b);
-    SEG_WAITVM(sg);
-    SEG_MARK(sg, 4);
+    SEG_IWAITVM(sg);
+    SEG_IMARK_DEP(sg, 4, rec_b.pr + rec_b.si + hop.x);
     const JField f = jones(rec_b, r);
 #else
     const JField f = jones(load_rec(B + kJBlockRec + 8 * b), r);
@@ -987,7 +1034,168 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     r.gy = mv.y;
     r.hr = hop.x;
     r.hi = hop.y;
-    SEG_MARK(sg, 5);
+    SEG_IMARK_DEP(sg, 5, r.er + r.ei + r.mr + r.mi + r.ener);
+    if (kind == 0) {
+        const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y, &K);
+        if (ba) return in_ic ? 0 : 2;
+        return in_ic ? 1 : kDie;
+    }
+    if (kind <= 2) return ba ? 2 : 3;
+    return ba ? 4 : 5;
+}
+
+// The same interaction in two halves, so that the wave issues ONE cell-word gather per pass for all
+// its lanes, between them (jones_body, WGRT_UNIFIED_CELL): interact_decide loads the block's line 0,
+// decides and moves the ray for a taken branch; the caller then loads the cell word of every lane that
+// moved (taken branches and miss hops) in one instruction; interact_take loads the taken matrix and hop
+// phasor and updates the field.  Each memory wait of a pass then covers every load the pass has in
+// flight: the line-0 wait the stores before it, the matrix wait every lane's new cell word -- where a
+// miss hop's gather issued in advance() used to hold up the line-0 wait of the lanes at an interaction
+// (vmcnt counts in issue order), and the next pass's advance() the stores of the out-coupling queue.
+// Amplification of the lanes' state discrepancy ("The bound, stated").  Both lanes apply
+// the same Jones matrix M to states that differ, up to a global phase, by a chordal distance eps; after the
+// normalisation the distance is at most a eps / (1 - eps / rho) (first order exact: a = |det M| |E|^2 /
+// |M E|^2, the stretch of the direction orthogonal to E over that of E; rho = |M E| / (sigma_max |E|)).
+// For a scaled-unitary M, a = 1; a singular one contracts (a = 0); a = kappa at worst, for the least
+// transmitted polarisation -- the branch the Monte-Carlo draw takes least often.  The Jones lane carries
+// A = prod max(1, a_k) (JRay::amp, times 1.006 per step for the second-order term and this evaluation's
+// rounding) and scales its certification bound by it; a branch with rho < 1e3 x the discrepancy bound is
+// abandoned (kUncertain).  WGRT_AMPLIFY=0 builds without it (the bound is then proven for
+// scaled-unitary matrices only, round 5).
+#ifndef WGRT_AMPLIFY
+#define WGRT_AMPLIFY 0
+#endif
+constexpr bool kAmplify = WGRT_AMPLIFY != 0;
+
+// |det M|^2 = det H, bounded from above from the tile's single-precision H = M^H M: the float products
+// are exact in double and the float entries carry 2^-24 relative rounding, so det H lies within
+// 7 2^-24 h11 h22 of this evaluation (|h12|^2 <= h11 h22).
+__device__ __forceinline__ double det2_ub(const float4 &h) {
+    const double hx = h.x, hy = h.y, hz = h.z, hw = h.w;
+    const double d = hx * hy - (hz * hz + hw * hw);
+    return fmax(d, 0.0) + 0x1p-21 * (hx * hy);
+}
+
+// The decision's half of a taken branch's amplification step, from the branch's H (single precision),
+// e2 = |E|^2 and q = the discrepancy bound the decision used (cert_tol (1 + G (n / 100)^2) amp):
+// pa = |det M|^2 |E|^4 (so a^2 = pa / |M E|^4), and nmin = 1e6 q^2 trace(H) |E|^2, the least |M E|^2 with
+// rho >= 1e3 q (sigma_max^2 <= trace H); both rounded up into floats.
+__device__ __forceinline__ void amp_prepare(const float4 &hb, double e2, double q, float &pa, float &nmin) {
+    pa = (float)(det2_ub(hb) * e2 * e2 * (1.0 + 0x1p-20));
+    nmin = (float)(1e6 * q * q * ((double)hb.x + (double)hb.y) * e2 * (1.0 + 0x1p-20));
+}
+
+// The take's half: amp times max(1, a) (rn = 1 / |M E| to ~1 ulp), or a negative value when |M E|^2 = n2
+// is below nmin (the first-order step is not certain there: the ray is abandoned).
+__device__ __forceinline__ float amp_step(float amp, float pa, float nmin, double n2, double rn) {
+    const double r2 = rn * rn;
+    const double a2 = (double)pa * r2 * r2;
+    float out = amp;
+    if (__builtin_expect(a2 > 1.0, 0)) out = (float)((double)amp * sqrt(a2) * 1.006);
+    return n2 < (double)nmin ? -1.0f : out;
+}
+
+struct JTake {
+    double cos_b;  // cosA_b: the next cos(theta)
+    double inv;    // 1 / cos(theta) (the taken branch's efficiency is n2 * cos_b * inv * f01, in that order)
+    double f01;    // n_g for the in-coupling event, else 1
+    double wb;     // SINGLE: the eerr increment's bound scale cert_tol * base * W[b] * 1.01
+    double2 hop;   // the new region's miss-hop phase step (loaded here, ahead of the caller's stores)
+    float pa;      // kAmplify: amp_prepare's |det M_b|^2 |E|^4 and least |M_b E|^2
+    float nmin;
+    bool ba;       // branch a (index 0) taken
+};
+
+template <bool SINGLE, class Loc>
+__device__ __forceinline__ int interact_decide(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
+                                               int kind, bool entry, JTake &tk, SegAcc *sg = nullptr) {
+    JRay &r = L.r;
+    const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
+    const double *B = T + kJHeader + kJBlock * blk;
+    const bool three = kind >= 3;
+    const bool thr = kind >= 1;
+    const double t = SINGLE ? A.threshold : 0.0;
+    const int ga = kind >= 3 ? 2 : 0;
+    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
+    double growth, cos_ic1;
+    const double4 cw = block_cw(B, entry, growth, cos_ic1);
+    const double2 mva = *(const double2 *)(T + kJGap + ga);
+    const double2 mvb = *(const double2 *)(T + kJGap + gb);
+    const double denom = entry ? cos_ic1 : r.cos_t;
+    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
+    const double inv = rcp_nr(denom);
+    const double f01 = entry ? A.n_g : 1.0;
+    const double nb = (double)L.bounces * 0.01;
+    const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
+    const double grow = kAmplify ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
+    const double base = grow * fabs(inv) * fmax(e2, 1.0);
+    JDecision d;
+    float4 h01[2];
+    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg, kAmplify ? h01 : nullptr);
+    jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
+    if (__builtin_expect(!d.ok, 0)) {
+        estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
+        jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
+    }
+    SEG_IMARK_DEP(sg, 3, d.a0 + d.a1 + d.a2 + (d.ok ? 1.0 : 0.0) + (d.s0 ? 2.0 : 0.0) + (d.s1 ? 4.0 : 0.0));
+    const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
+    const bool ba = d.s0;
+    if (kAmplify) amp_prepare(ba ? h01[0] : h01[1], e2, A.cert_tol * grow, tk.pa, tk.nmin);
+    const double2 mv = ba ? mva : mvb;
+    tk.ba = ba;
+    tk.cos_b = ba ? cw.x : cw.y;
+    tk.inv = inv;
+    tk.f01 = f01;
+    tk.wb = SINGLE ? A.cert_tol * base * B[kJBlockW + (ba ? 0 : 1)] * 1.01 : 0.0;
+    if (code == 0) {   // the taken branch's new position (its cell word: the caller's gather)
+        r.x = r.x + mv.x;
+        r.y = r.y + mv.y;
+        r.gx = mv.x;
+        r.gy = mv.y;
+        // issued here, before the caller's queue and retire stores, so neither the compiler nor the
+        // in-order wait puts it behind the matrix (it is read by the next pass's miss hop)
+        tk.hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
+    }
+    return code;
+}
+
+// The taken branch's second half (after the caller's gather of L.pf at the new position): the field,
+// ener, the next region.  kUncertain for a field too small to normalise.
+template <bool SINGLE, class Loc>
+__device__ __forceinline__ int interact_take(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
+                                             int kind, const JTake &tk, SegAcc *sg = nullptr) {
+    JRay &r = L.r;
+    const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
+    const double *B = T + kJHeader + kJBlock * blk;
+    const bool ba = tk.ba;
+    const double2 hop = tk.hop;
+#ifdef WGRT_SEG
+    const Rec rec_b = load_rec(B + kJBlockRec + (ba ? 0 : 8));
+    SEG_IWAITVM(sg);
+    SEG_IMARK_DEP(sg, 4, rec_b.pr + rec_b.si + hop.x);
+    const JField f = jones(rec_b, r);
+#else
+    const JField f = jones(load_rec(B + kJBlockRec + (ba ? 0 : 8)), r);
+#endif
+    const double n2 = norm2(f);
+    if (!(n2 > 1e-300)) return kUncertain;
+    const double rn = rsq_nr(n2);
+    if (kAmplify) {
+        const float a = amp_step(r.amp, tk.pa, tk.nmin, n2, rn);
+        if (__builtin_expect(a < 0.0f, 0)) return kUncertain;
+        r.amp = a;
+    }
+    r.er = f.er * rn;
+    r.ei = f.ei * rn;
+    r.mr = f.mr * rn;
+    r.mi = f.mi * rn;
+    const double ab = n2 * tk.cos_b * tk.inv * tk.f01;   // interact()'s association
+    if (SINGLE) r.eerr += tk.wb * rcp_nr(ab) + 1e-15;
+    r.ener = r.ener * ab;
+    r.cos_t = tk.cos_b;
+    r.hr = hop.x;
+    r.hi = hop.y;
+    SEG_IMARK_DEP(sg, 5, r.er + r.ei + r.mr + r.mi + r.ener);
     if (kind == 0) {
         const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y, &K);
         if (ba) return in_ic ? 0 : 2;
@@ -1033,8 +1241,11 @@ __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); 
 // evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
-template <class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind) {
+// UNI (WGRT_UNIFIED_CELL): a miss hop does not load its cell word here; it sets `reload` and the caller's
+// one gather per pass loads it (with the taken branches' cell words, after the decisions).
+template <bool UNI = false, class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind,
+                                       bool *reload = nullptr) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
@@ -1083,8 +1294,9 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
         const double mr = r.mr;
         r.mr = fma(mr, r.hr, -r.mi * r.hi);
         r.mi = fma(mr, r.hi, r.mi * r.hr);
-        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
+        if (!UNI) L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
+    if (UNI) *reload = hop;
     const int step = hit ? blkbase + sl : kTransit;
     const int next = ic ? 1 + region : step;
     return die ? kDie : next;
@@ -1103,12 +1315,14 @@ __device__ __forceinline__ uint64_t wave_sum(uint64_t v) {
 
 // Per-wave reduction of the ray counters, then one 64-bit atomic per counter per wave.
 __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t bounces, uint64_t hits,
-                                          uint64_t bad, uint64_t inter) {
+                                          uint64_t bad, uint64_t inter, uint64_t libm = 0) {
     bounces = wave_sum(bounces);
     hits = wave_sum(hits);
     bad = wave_sum(bad);
     inter = wave_sum(inter);
+    libm = wave_sum(libm);
     if ((threadIdx.x & 63) == 0 && stats) {
+        if (libm) atomicAdd((unsigned long long *)&stats->libm_rays, (unsigned long long)libm);
         if (inter) atomicAdd((unsigned long long *)&stats->interactions, (unsigned long long)inter);
         if (bounces) atomicAdd((unsigned long long *)&stats->bounces, (unsigned long long)bounces);
         if (hits) atomicAdd((unsigned long long *)&stats->eyebox_hits, (unsigned long long)hits);
@@ -1120,7 +1334,7 @@ __device__ __forceinline__ void add_stats(wgrt_trace_stats *stats, uint64_t boun
 // s_io, the trace starts from *s_io instead of rng_states[i] and leaves its final state there
 // (rng_states untouched).  ni (optional) counts the interactions after the in-coupling event.
 __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_t &b, uint64_t &h, uint64_t &bad,
-                                          uint32_t *s_io = nullptr, uint64_t *ni = nullptr) {
+                                          uint32_t *s_io = nullptr, uint64_t *ni = nullptr, uint64_t *lm = nullptr) {
     Lane L;
     if (!lane_load(A, i, L)) {
         ++bad;
@@ -1142,6 +1356,7 @@ __device__ __forceinline__ void trace_one(const TraceArgs &A, int64_t i, uint64_
     else lane_retire(A, L);
     b += L.bounces;
     h += L.hit;
+    if (lm) *lm += L.libm ? 1u : 0u;
 }
 
 }  // namespace wgrt

@@ -72,9 +72,9 @@ constexpr double kDefaultCellMm = WGRT_CELL_MM;
 // Variant 1: one ray per lane over a 1-D grid (the reference's launch shape, MAIN:167).
 __global__ __launch_bounds__(256) void trace_grid_kernel(TraceArgs A) {
     const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
-    uint64_t b = 0, h = 0, bad = 0, ni = 0;
-    if (i < A.n_rays) trace_one(A, i, b, h, bad, nullptr, &ni);
-    add_stats(A.stats, b, h, bad, ni);
+    uint64_t b = 0, h = 0, bad = 0, ni = 0, lm = 0;
+    if (i < A.n_rays) trace_one(A, i, b, h, bad, nullptr, &ni, &lm);
+    add_stats(A.stats, b, h, bad, ni, lm);
 }
 
 // Launch scratch counters of the Jones-vector variants: kHeads work-queue heads, then the replay
@@ -88,11 +88,20 @@ constexpr int kScratchCtr = (kHeads + 5) * kHeadStride;   // heads, replay / que
 // replays chain the traces after an abandoned one): every wave bins the out-coupling blocks it filled
 // when it ends (a chain of block links, its own stores), every workgroup adds its counter totals with
 // agent-scope atomics and counts itself done, and the workgroup that counts last adds the totals to
-// *stats and zeroes the next launch's counter set.  Abandoned rays are re-traced by replay_kernel
-// behind the launch, which reads one count and leaves when there are none.  A replay call inside the
-// trace kernel (a non-inlined trace_one) gave the wave loop 128 VGPRs and 536 B of scratch per lane and
-// lost 14-27 %; this design gains 1-4 % on single launches.  WGRT_INKERNEL_EPI=0
-// builds the epilogue-kernel design for single launches too.
+// *stats, zeroes the next launch's counter set and re-traces the abandoned rays (an inlined trace_one
+// whose arguments are read from the kernarg segment there: replay_tail; none in practice).  A non-inlined
+// trace_one call gave the wave loop 128 VGPRs and 536 B of scratch per lane and lost 14-27 %; the
+// inlined one costs SGPR spills outside the loop only (round 6).  WGRT_INKERNEL_EPI=0 builds the
+// epilogue-kernel design for single launches too.
+//
+// The hand-off to the last workgroup is MI355X_MICROARCH.md's measured form "one lane of each storing
+// workgroup signals with an agent-scope atomic add after every storing wave's vmcnt(0) wait; the
+// workgroup whose add came last loads with sc1 (agent-scope) loads": the totals are agent-scope atomics,
+// the replay-list entries agent-scope stores each waited for by its lane, and the last workgroup reads
+// both with agent-scope loads.  A release / acquire pair on the done count would add an L2 write-back
+// and an L1 invalidate per workgroup (the guide prices them at ~1.7 us each), so the order rests on the
+// explicit s_waitcnt vmcnt(0), which on gfx950 covers stores and no-return atomics (GFX9 has no
+// separate store counter; this file targets gfx950 only).
 #ifndef WGRT_INKERNEL_EPI
 #define WGRT_INKERNEL_EPI 1
 #endif
@@ -118,11 +127,11 @@ constexpr int kQBlock = WGRT_QBLOCK;    // out-coupling queue slots a wave reser
 static_assert(kQBlock >= 1 && kQBlock <= 64, "a queue block is binned by one lane per entry");
 
 __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
-    __shared__ unsigned long long red[4][5];
+    __shared__ unsigned long long red[4][6];
     const unsigned long long nr = *A.replay_count, nf = *A.full_count;
     const unsigned long long tid = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x;
     const unsigned long long nth = (unsigned long long)gridDim.x * blockDim.x;
-    uint64_t h = 0, b = 0, bad = 0, gu = 0, ni = 0;
+    uint64_t h = 0, b = 0, bad = 0, gu = 0, ni = 0, lm = 0;
     for (unsigned long long e = tid; e < nf * kQBlock; e += nth) {
         {
             const unsigned long long j = (unsigned long long)A.full_list[e / kQBlock] * kQBlock + e % kQBlock;
@@ -136,11 +145,11 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     for (unsigned long long k = tid; k < nr; k += nth) {
         const int64_t i = (int64_t)A.replay_list[k];
         if (A.n_iter <= 1) {
-            trace_one(A, i, b, h, bad, nullptr, &ni);
+            trace_one(A, i, b, h, bad, nullptr, &ni, &lm);
         } else {   // fused launch: the traces from the abandoned one to the last, chained
             const uint64_t w = A.rng64[i];
             uint32_t st = (uint32_t)(w >> 32);
-            for (int it = (int)(w & 0xffu); it < A.n_iter; ++it) trace_one(A, i, b, h, bad, &st, &ni);
+            for (int it = (int)(w & 0xffu); it < A.n_iter; ++it) trace_one(A, i, b, h, bad, &st, &ni, &lm);
             A.rng[i] = st;
         }
     }
@@ -161,12 +170,14 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
     h = wave_sum(h);
     gu = wave_sum(gu);
     ni = wave_sum(ni);
+    lm = wave_sum(lm);
     if ((threadIdx.x & 63) == 0) {
         red[w][0] = b;
         red[w][1] = bad;
         red[w][2] = h;
         red[w][3] = gu;
         red[w][4] = ni;
+        red[w][5] = lm;
     }
     __syncthreads();
     if (threadIdx.x == 0 && A.stats) {
@@ -176,7 +187,9 @@ __global__ __launch_bounds__(256) void epilogue_kernel(TraceArgs A) {
         const unsigned long long t2 = red[0][2] + red[1][2] + red[2][2] + red[3][2];
         const unsigned long long t3 = red[0][3] + red[1][3] + red[2][3] + red[3][3];
         const unsigned long long t4 = red[0][4] + red[1][4] + red[2][4] + red[3][4];
+        const unsigned long long t5 = red[0][5] + red[1][5] + red[2][5] + red[3][5];
         if (t4) atomicAdd((unsigned long long *)&st->interactions, t4);
+        if (t5) atomicAdd((unsigned long long *)&st->libm_rays, t5);
         if (t0) atomicAdd((unsigned long long *)&st->bounces, t0);
         if (t1) atomicAdd((unsigned long long *)&st->bad_rays, t1);
         if (t2) atomicAdd((unsigned long long *)&st->eyebox_hits, t2);
@@ -196,6 +209,22 @@ constexpr int kFusedRefill = 16;
 #define WGRT_STRIPE 16
 #endif
 constexpr int64_t kStripe = WGRT_STRIPE;
+// -DWGRT_SEG=2: wave-uniform segment marks at the top level of a pass (tools/segments.py)
+#if defined(WGRT_SEG) && WGRT_SEG == 2
+#define SEG_TMARK(sg, k, dep) SEG_MARK_DEP(sg, k, dep)
+#else
+#define SEG_TMARK(sg, k, dep) ((void)0)
+#endif
+
+// One cell-word gather per pass for every lane that moved (taken branches and miss hops), issued after
+// the decisions (wgrt_device.h interact_decide / interact_take).
+#ifndef WGRT_UNIFIED_CELL
+#define WGRT_UNIFIED_CELL 0
+#endif
+constexpr bool kUnifiedCell = WGRT_UNIFIED_CELL != 0;
+#ifndef WGRT_LATE_RETIRE
+#define WGRT_LATE_RETIRE 1
+#endif
 #ifndef WGRT_ONE_RETIRE
 #define WGRT_ONE_RETIRE 1
 #endif
@@ -237,8 +266,11 @@ __device__ __forceinline__ uint32_t iter_tag(uint32_t epoch, uint32_t k, bool br
     return (epoch << 9) | (broken ? 0x100u : 0u) | k;
 }
 
+// Single launches re-trace their abandoned rays inside the trace kernel (the workgroup that counts
+// itself done last: replay_tail), so no replay kernel follows the launch: -0.2 to -1.6 % per single
+// launch.  WGRT_INKERNEL_REPLAY=0 builds the round-5 design (replay_kernel behind it).
 #ifndef WGRT_INKERNEL_REPLAY
-#define WGRT_INKERNEL_REPLAY 0
+#define WGRT_INKERNEL_REPLAY 1
 #endif
 
 // An abandoned ray (kUncertain) onto the replay list.  With the in-kernel replay the entry is stored at
@@ -277,11 +309,11 @@ __device__ WGRT_REPLAY_INL void replay_tail(const KArgs &K, unsigned long long n
     R.loc.row_off = KLOC(row_off); R.loc.row_edges = KLOC(row_edges); R.loc.bands = KLOC(bands);
     R.loc.x0 = KLOC(x0); R.loc.y0 = KLOC(y0); R.loc.inv_h = KLOC(inv_h); R.loc.ncx = KLOC(ncx); R.loc.ncy = KLOC(ncy);
     const uint32_t *const list = KA(replay_list);
-    uint64_t b = 0, h = 0, bad = 0, ni = 0;
+    uint64_t b = 0, h = 0, bad = 0, ni = 0, lm = 0;
     for (unsigned long long k = threadIdx.x; k < nr; k += blockDim.x)
         trace_one(R, (int64_t)__hip_atomic_load(list + k, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT), b, h, bad,
-                  nullptr, &ni);
-    add_stats(R.stats, b, h, bad, ni);
+                  nullptr, &ni, &lm);
+    add_stats(R.stats, b, h, bad, ni, lm);
     if (threadIdx.x == 0 && R.stats) atomicAdd((unsigned long long *)&R.stats->replayed, nr);
 }
 #endif
@@ -306,6 +338,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // that ended in the previous pass's interaction and those advance() ends (fused launches retire at
     // once: their hand-off would wait a pass)
     constexpr bool ONE = !FUSED && kOneRetire;
+    constexpr bool UNI = kUnifiedCell;
     bool fin = false;
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
@@ -333,6 +366,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
+    bool reload = false;   // UNI: this lane's miss hop moved it; its cell word is loaded in interact_pass
     // per-lane totals in 32 bits: a lane's bounce total is added to the stats directly before it
     // could overflow (2^31 bounces on one lane: never in practice)
     uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0, tot_int = 0;
@@ -445,41 +479,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // the second half of a pass: the interaction of the lanes at one, then this pass's
     // out-couplings into the wave's block of queue slots (a contended returning atomic per pass
     // would put its latency on every pass; a new block is needed about once per hundred passes)
-    auto interact_pass = [&](SegAcc *sg) {
-        if (TL && tl_on) {
-            ++tl_passes;
-            tl_lanes += __popcll(__ballot(active));
-        }
-        bool out = false;
-        if (active && blk >= 0) {
-            L.inter += entry ? 0u : 1u;
-            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
-            if (ONE) {
-                // straight-line: a trace that ended (out-coupled or died) is retired at the next
-                // pass's retire site; an abandoned one (rare) goes to the replay list
-                out = next == kOut;
-                fin = (next < 0) & (next != kUncertain);
-                active = next >= 0;
-                L.r.region = next >= 0 ? next : L.r.region;
-                if (__builtin_expect(next == kUncertain, 0)) record_abandoned(K, L.i);
-            } else {
-                // one retire site for both ends of a trace (out-coupled, died)
-                out = next == kOut;
-                L.r.region = next >= 0 ? next : L.r.region;
-                if (__builtin_expect(next == kUncertain, 0)) {
-                    // abandoned with no side effect; replay_kernel re-traces it (fused: epilogue_kernel,
-                    // from this iteration on, so later iterations skip the ray)
-                    if (FUSED)
-                        __hip_atomic_store(KA(rng64) + L.i,
-                                           ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
-                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-                    record_abandoned(K, L.i);
-                    active = false;
-                } else if (next < 0) {
-                    retire();
-                }
-            }
-        }
+    // this pass's out-couplings into the wave's block of queue slots (a contended returning atomic per
+    // pass would put its latency on every pass; a new block is needed about once per hundred passes)
+    auto queue_out = [&](bool out) {
         const uint64_t om = __ballot(out);
         if (om != 0ull) {
             const int nout = __popcll(om), rem = kQBlock - qfill;
@@ -519,12 +521,81 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 qfill += nout;
             }
         }
+    };
+    // the outcome of an interaction (next region, or kDie / kOut / kUncertain): retire bookkeeping
+    auto outcome = [&](int next) {
+        if (ONE) {
+            // straight-line: a trace that ended (out-coupled or died) is retired at the next
+            // pass's retire site; an abandoned one (rare) goes to the replay list
+            fin = (next < 0) & (next != kUncertain);
+            active = next >= 0;
+            L.r.region = next >= 0 ? next : L.r.region;
+            if (__builtin_expect(next == kUncertain, 0)) record_abandoned(K, L.i);
+        } else {
+            // one retire site for both ends of a trace (out-coupled, died)
+            L.r.region = next >= 0 ? next : L.r.region;
+            if (__builtin_expect(next == kUncertain, 0)) {
+                // abandoned with no side effect; the replay re-traces it (fused: epilogue_kernel,
+                // from this iteration on, so later iterations skip the ray)
+                if (FUSED)
+                    __hip_atomic_store(KA(rng64) + L.i,
+                                       ((uint64_t)L.s0 << 32) | iter_tag(A.iter_epoch, L.k, true),
+                                       __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                record_abandoned(K, L.i);
+                active = false;
+            } else if (next < 0) {
+                retire();
+            }
+        }
+    };
+
+    // the second half of a pass: the interaction of the lanes at one, and this pass's out-couplings.
+    // UNI: decide, queue the out-couplings, load the new cell word of every lane that moved (taken
+    // branches and miss hops: one gather instruction), then the taken branches' matrices.
+    auto interact_pass = [&](SegAcc *sg, bool late_retire) {
+        if (TL && tl_on) {
+            ++tl_passes;
+            tl_lanes += __popcll(__ballot(active));
+        }
+        if (UNI) {
+            const bool inter = active && blk >= 0;
+            JTake tk;
+            int next = 0;
+            if (inter) {
+                L.inter += entry ? 0u : 1u;
+                next = interact_decide<SINGLE>(A, K, loc, L, blk, kind, entry, tk, sg);
+            }
+            SEG_TMARK(sg, 2, (double)next);
+            queue_out(inter && next == kOut);
+            if (late_retire && fin) {   // (launch tail: its stores go out behind the line-0 wait)
+                retire();
+                fin = false;
+            }
+            SEG_TMARK(sg, 3, 0.0);
+            const bool take = inter && next == 0;
+            if (take || (active && reload)) L.pf = locate_c(loc, L.r.x, L.r.y);   // read by the next pass
+            SEG_TMARK(sg, 4, 0.0);
+            if (take) next = interact_take<SINGLE>(A, K, loc, L, blk, kind, tk, sg);
+            SEG_TMARK(sg, 5, L.r.er + (double)next);
+            if (inter) outcome(next);
+        } else {
+            bool out = false;
+            if (active && blk >= 0) {
+                L.inter += entry ? 0u : 1u;
+                const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
+                out = next == kOut;
+                outcome(next);
+            }
+            SEG_TMARK(sg, 5, L.r.er);
+            queue_out(out);
+        }
         SEG_MARK(sg, 6);
     };
 
     for (;;) {
+        reload = false;
         if (active) {
-            blk = advance(A, K, loc, L, kind);
+            blk = advance<UNI>(A, K, loc, L, kind, &reload);
             entry = false;
             if (ONE) fin |= blk == kDie;
             else if (blk == kDie) retire();
@@ -643,7 +714,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
         // the tail loop below
         if (!FUSED && exhausted) break;
-        interact_pass(nullptr);
+        interact_pass(nullptr, false);
     }
     if (!FUSED && __ballot(active) != 0ull) {
         // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
@@ -653,37 +724,51 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // 1.5 % and 6 %: the chip is still full of rays when the queue runs dry.
         // The first pass continues the one the main loop broke off (advance and refill done).
 #ifdef WGRT_SEG
-        SegAcc seg{};
-        SegAcc *const sg = (TL && tl_on) ? &seg : nullptr;
+        __shared__ uint32_t seg_lds[4][16];
+        SegAcc seg{(uint32_t __attribute__((address_space(3))) *)&seg_lds[threadIdx.x >> 6][0]};
+        if (lane < 9) seg.p[lane] = 0u;
+        SegAcc *const sg = TL ? &seg : nullptr;   // compile-time: the stamps are straight-line code
 #else
         SegAcc *const sg = nullptr;
 #endif
+        // UNI single launches retire the rays that ended inside interact_pass, after the line-0 loads, so
+        // that the retire stores do not hold up the line-0 wait (vmcnt counts stores in issue order)
+        constexpr bool LATE = ONE && UNI && WGRT_LATE_RETIRE;
         for (bool first = true;; first = false) {
 #ifdef WGRT_SEG
-            if (sg) seg.last = seg_stamp();
+            if (sg) {
+                const uint32_t t0 = seg_stamp();
+                if (seg_first_lane()) seg.p[8] = t0;
+            }
 #endif
+            // (the first pass continues the main loop's: its miss hops' reload flags stand)
+            if (!first) reload = false;
             if (!first && active) {
-                blk = advance(A, K, loc, L, kind);
+                blk = advance<UNI>(A, K, loc, L, kind, &reload);
                 entry = false;
                 if (ONE) fin |= blk == kDie;
                 else if (blk == kDie) retire();
             }
-            SEG_MARK(sg, 0);
-            if (ONE && fin) {
+            SEG_MARK_DEP(sg, 0, (double)blk + L.r.x);
+            if (ONE && !LATE && fin) {
                 retire();
                 fin = false;
             }
             if (__ballot(active) == 0ull) break;
             SEG_MARK(sg, 1);
 #ifdef WGRT_SEG
-            seg.s[7] += 1;
+            if (seg_first_lane()) seg.p[7] += 1u;
 #endif
-            interact_pass(sg);
+            interact_pass(sg, LATE);
+        }
+        if (LATE && fin) {   // ended in the last pass's interaction
+            retire();
+            fin = false;
         }
 #ifdef WGRT_SEG
         // segment sums: words 8..15 of a 16-word wave record (tools/segments.py)
-        if (sg && lane == 0)
-            for (int k = 0; k < 8; ++k) tl[kTlWords * tl_wave + 8 + k] = seg.s[k];
+        if (TL && tl_on && lane == 0)
+            for (int k = 0; k < 8; ++k) tl[kTlWords * tl_wave + 8 + k] = seg.p[k];
 #endif
     }
     // the block this wave holds is binned by the wave itself (GRTF:1162-1171, 1231-1240): one
@@ -795,11 +880,11 @@ constexpr int kReplayGroups = 64;
 __global__ __launch_bounds__(256) void replay_kernel(TraceArgs A) {
     const unsigned long long nr = *A.replay_count;
     if (nr == 0ull) return;
-    uint64_t b = 0, h = 0, bad = 0, ni = 0;
+    uint64_t b = 0, h = 0, bad = 0, ni = 0, lm = 0;
     for (unsigned long long k = (unsigned long long)blockIdx.x * blockDim.x + threadIdx.x; k < nr;
          k += (unsigned long long)gridDim.x * blockDim.x)
-        trace_one(A, (int64_t)A.replay_list[k], b, h, bad, nullptr, &ni);
-    add_stats(A.stats, b, h, bad, ni);
+        trace_one(A, (int64_t)A.replay_list[k], b, h, bad, nullptr, &ni, &lm);
+    add_stats(A.stats, b, h, bad, ni, lm);
     if (blockIdx.x == 0 && threadIdx.x == 0 && A.stats) atomicAdd((unsigned long long *)&A.stats->replayed, nr);
 }
 
@@ -1583,7 +1668,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         // fused launches keep the epilogue kernel (their replays chain the traces after the abandoned one)
         if (num_iter > 1 || !kInKernelEpilogue)
             hipLaunchKernelGGL(epilogue_kernel, dim3(kEpilogueGroups), dim3(256), 0, st, A);
-        else if (!WGRT_INKERNEL_REPLAY || timeline)   // (the timeline kernels keep the replay kernel)
+        else if (!WGRT_INKERNEL_REPLAY)   // else the last trace workgroup replays (jones_body)
             hipLaunchKernelGGL(replay_kernel, dim3(kReplayGroups), dim3(256), 0, st, A);
         e = hipGetLastError();
     }

@@ -60,7 +60,7 @@ def trace_fullcolor(scene: Scene, rays: dict, rng_states: torch.Tensor, matrix_E
     (``x, y, m, n, lmd_num, te, tm, delta_phase`` required; the four columns the
     kernel never reads may be absent).  rng_states uint32 -> torch.int32 view is
     accepted too.  stats: optional int64[STATS_LEN] device tensor that is added to
-    (bounces, bad_rays, eyebox_hits, replayed, handoff_giveups, interactions; ``check_stats`` raises
+    (bounces, bad_rays, eyebox_hits, replayed, handoff_giveups, interactions, libm_rays; ``check_stats`` raises
     on a hand-off give-up).  chunk_order: optional int32 device permutation of the 64-ray chunks
     (``schedule_by_lifetime``); results do not depend on it.  num_iter: chained traces of every
     ray (the reference's ``num_iter`` loop of launches, MAIN:169-177) in one call -- results
@@ -86,11 +86,23 @@ def new_stats(device) -> torch.Tensor:
 
 def check_stats(stats: torch.Tensor) -> None:
     """Raise if a fused launch gave up a hand-off (``wgrt_trace_stats.handoff_giveups``): the
-    eyebox grid and RNG states of that call are then wrong (synchronises on ``stats``)."""
-    g = int(stats[4].item())
+    eyebox grid and RNG states of that call are then wrong.  Warn (``luts.EnerUnderflowWarning``, a
+    ``LUTPrecisionWarning``) if traces were decided in the ener-underflow regime
+    (``wgrt_trace_stats.libm_rays``, ABI 7): their paths depend on the libm's last bits, so they may
+    differ from a CPU run of the reference.  Synchronises on ``stats``."""
+    st = stats.cpu()
+    g = int(st[4])
     if g:
         raise WgrtError(f"{g} fused-launch traces gave up waiting for their ray's previous trace "
                         "(hand-off failure; results of this call are invalid)")
+    lm = int(st[6]) if st.numel() > 6 else 0
+    if lm:
+        import warnings
+        from .luts import EnerUnderflowWarning
+        warnings.warn(f"{lm} traces reached the ener-underflow regime (a guard product ener * e below 2^-1000, "
+                      "GRTF:1020): their decisions hang on the last bits of cos / sin / atan2, so they may differ "
+                      "from the reference run on another libm (wgrt_trace_stats.libm_rays)",
+                      EnerUnderflowWarning, stacklevel=2)
 
 
 def reserve(scene: Scene, n_rays: int, num_iter: int = 1, stream=None) -> None:

@@ -207,6 +207,12 @@ class LUTPrecisionWarning(UserWarning):
     """A LUT was given in single precision (complex64 / float32)."""
 
 
+class EnerUnderflowWarning(LUTPrecisionWarning):
+    """Traces were decided in the ener-underflow regime (``wgrt_trace_stats.libm_rays``, ABI 7): a LUT
+    whose rays live so long without loss that ``ener = prod(e)`` nears the subnormal range, where the
+    full-colour guard ``ener * e > 0`` (GRTF:1020) depends on the libm's last bits."""
+
+
 def lut_f32_mask(luts: dict) -> int:
     """wgrt_scene_opts.lut_f32_angles of a LUT set as given: bit k for each table k (ic1, ic2, ic3,
     fc1, fc2, oc1, oc2) held in single precision.  The reference loads the .npy files as stored

@@ -43,7 +43,7 @@
 extern "C" {
 #endif
 
-#define WGRT_ABI_VERSION 6
+#define WGRT_ABI_VERSION 7
 
 typedef enum {
     WGRT_OK = 0,
@@ -111,6 +111,14 @@ typedef struct {
                                   GRTF:905 that draw: coupler hits in R0..R5).  The other bounces are the
                                   in-coupling events (one per traced ray, GRTF:860-904) and the iterations
                                   without a draw: miss hops, R3 -> R4 switches, terminations.          */
+    uint64_t libm_rays;        /* ABI 7.  Traces decided in the ener-underflow regime: a guard product
+                                  ener * e_k (GRTF:1020, 1073, 1136, ...) of a nonzero efficiency fell below
+                                  2^-1000, where whether it rounds to zero -- and so the ray's path --
+                                  depends on the last bits of cos / sin / atan2 (glibc vs the device libm),
+                                  not on the reference's formula alone.  Such traces are decided by the
+                                  reference arithmetic (the Jones-vector lane abandons them to it), and
+                                  are counted here; the Python layer warns (LUTPrecisionWarning) when the
+                                  count is nonzero.  0 on every BASELINE configuration. */
 } wgrt_trace_stats;
 
 typedef struct {

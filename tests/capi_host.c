@@ -10,7 +10,7 @@
  * IN (written by tests/test_capi_host.py): a sequence of records, each an int64 element count
  * followed by the elements, in the order read below (geometry, LUTs as interleaved complex128,
  * the scalar block, the eight float32 ray columns the kernel reads, the uint32 RNG states).
- * OUT: rng_states after the launches (uint32[n]), matrix_EB (float32), wgrt_trace_stats (6 x u64).
+ * OUT: rng_states after the launches (uint32[n]), matrix_EB (float32), wgrt_trace_stats (7 x u64, ABI 7).
  * Exit status 0 on success; a failing call prints wgrt_last_error() and exits 2.
  * Built by __graft_entry__.build() (gcc, tests/_capi.py) into tests/bin/; no torch, no Python.
  */

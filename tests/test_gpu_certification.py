@@ -144,7 +144,7 @@ def test_certification_slack(dev, name, cfg):
     ("adv_lossless_long", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_lossless",
                                gap_scale=0.05, tir_near_pi=True)),
 ])
-@pytest.mark.parametrize("variant", [7, 9])
+@pytest.mark.parametrize("variant", [7, 9, 1])
 def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
     """The product kernel on the adversarial LUTs, two chained launches, against the CPU oracle:
     per-ray bounces, RNG states and the eyebox grid bit for bit (through the certified decisions and
@@ -157,7 +157,11 @@ def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
     nudged by one ulp; compiled Numba on a GPU (libdevice) would differ from the reference's CPU run
     there too.  The oracle's event-hook build flags every ray that reaches a guard product below
     2^-1000 (``underflow=True``); those rays, and the eyebox slabs they (or an H6 spill from the slab
-    before) write, are left out of the bit-exact comparison, and every mismatch must be such a ray."""
+    before) write, are left out of the bit-exact comparison, and every mismatch must be such a ray.
+
+    ABI 7: the product counts the traces it decided in that regime (``wgrt_trace_stats.libm_rays``, from
+    the reference-arithmetic lane that decides them) -- at least every ray that newly mismatches the oracle
+    in a launch, and ``engine.check_stats`` warns (``EnerUnderflowWarning``) when the count is nonzero."""
     from oracle import OracleScene
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import (Scene, init_rays, new_stats,
                                                                            trace_fullcolor)
@@ -175,6 +179,7 @@ def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import slab_ids
     N = hr["x"].shape[0]
     flagged = np.zeros(N, dtype=bool)
+    prev_bad = np.zeros(N, dtype=bool)
     for it in range(2):
         per = torch.zeros(rng.numel(), dtype=torch.int32, device=dev)
         st = new_stats(dev)
@@ -186,6 +191,15 @@ def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
         g_cnt, g_rng = per.cpu().numpy().view(np.uint32), rng.cpu().numpy().view(np.uint32)
         bad = (g_cnt != cnt) | (g_rng != orng)
         assert not (bad & ok).any(), (name, it, np.nonzero(bad & ok)[0][:20])
+        # every ray whose trace diverged in this launch was counted as decided in the underflow regime
+        libm = int(st[6])
+        assert libm >= int((bad & ~prev_bad).sum()), (name, it, libm, int((bad & ~prev_bad).sum()))
+        if libm:
+            from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import check_stats
+            from gpu_ray_tracing_for_waveguide_based_ar_display_amd.luts import EnerUnderflowWarning
+            with pytest.warns(EnerUnderflowWarning):
+                check_stats(st)
+        prev_bad = bad
         # eyebox slabs written only by libm-determined rays (and not reached by a flagged slab's spill)
         blocks = np.arange(N // R)
         s_all = slab_ids(blocks, nx, ny, lam)
@@ -198,7 +212,7 @@ def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
         if not flagged.any():
             assert int(st[0]) == tot
         print(name, variant, "launch", it, "rays flagged (ener underflow):", int(flagged.sum()),
-              "mismatching:", int(bad.sum()))
+              "mismatching:", int(bad.sum()), "libm_rays:", libm)
     scene.close()
 
 
@@ -232,6 +246,7 @@ def _blocks_vs_oracle(dev, nx, ny, lambdas, R, sample, profile="default", thread
         m, n = divmod(fov, ny)
         l = lambdas[k]
         np.testing.assert_array_equal(eb[l, n, m].cpu().numpy(), oeb[l, n, m], err_msg=f"block {b} slab")
+    assert int(stats[6]) == 0, int(stats[6])   # no trace in the ener-underflow regime (libm_rays, ABI 7)
     return int(stats[0]), int(stats[3])
 
 
@@ -263,3 +278,20 @@ def test_main_default_job_matches_oracle_on_blocks(dev):
     bounces, replayed = _blocks_vs_oracle(dev, 100, 75, [0, 1, 2], 5000, sample)
     assert bounces > 112_500_000
     _record("main_default_blocks_vs_oracle", {"blocks": len(sample), "gpu_bounces": bounces, "replayed": replayed})
+
+
+@pytest.mark.parametrize("R", [1024, 4096])   # C3, C4
+def test_no_underflow_regime_on_baseline_configs(dev, R):
+    """ABI 7 ``libm_rays`` is 0 on the BASELINE configs: every trace of C3 and C4, run through the
+    reference-arithmetic lane (variant 1, which evaluates every guard product), stays clear of the
+    ener-underflow regime, so no result there depends on the libm's last bits."""
+    from gpu_ray_tracing_for_waveguide_based_ar_display_amd.engine import Scene, init_rays, new_stats, trace_fullcolor
+    geom, luts, pts = _setup(21, 21, [0, 1, 2], R)
+    scene = Scene.from_geometry(geom, luts)
+    rays, rng = init_rays(pts, 21, 21, [0, 1, 2], R, device=dev, all_columns=False)
+    eb = torch.zeros(scene.eb_shape(), dtype=torch.float32, device=dev)
+    st = new_stats(dev)
+    trace_fullcolor(scene, rays, rng, eb, stats=st, variant=1)
+    torch.cuda.synchronize()
+    assert int(st[0]) > 0 and int(st[6]) == 0, st.cpu().tolist()
+    scene.close()

@@ -102,7 +102,7 @@ def main():
             env = dict(os.environ, REPO=REPO, AB_CONFIG=a.config, AB_LAUNCHES=str(a.launches),
                        AB_FUSED=str(a.fused), AB_ORDER=order, AB_SCENE=json.dumps(scene_kw),
                        AB_LAUNCH=json.dumps(launch_kw), AB_PROFILE=a.profile, AB_SHARD=str(a.shard))
-            p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "with_lib.py"), lib, "--abi", "4,5,6", "-c",
+            p = subprocess.run([sys.executable, os.path.join(REPO, "tools", "with_lib.py"), lib, "--abi", "4,5,6,7", "-c",
                                 CHILD], env=env, capture_output=True, text=True, timeout=300)
             if p.returncode:
                 print(p.stderr[-3000:])
