@@ -95,7 +95,7 @@ class ShadowStats(ctypes.Structure):
                 ("bounces", ctypes.c_uint64), ("fallbacks", ctypes.c_uint64), ("max_ratio", ctypes.c_double),
                 ("max_ratio32", ctypes.c_double),
                 ("max_ratio_by_depth", ctypes.c_double * 6), ("decisions_by_depth", ctypes.c_uint64 * 6),
-                ("ratio_hist", ctypes.c_uint64 * 20), ("max_ener_ratio", ctypes.c_double)]
+                ("ratio_hist", ctypes.c_uint64 * 20), ("max_ener_ratio", ctypes.c_double), ("max_amp", ctypes.c_double)]
 
 
 class SceneInfo(ctypes.Structure):

@@ -897,12 +897,16 @@ __device__ __forceinline__ void jones_decide(JDecision &d, double u, double scl,
 // The same loads also bring what the tile header would otherwise be loaded for: the phase-growth bound,
 // and for block 0 (entry: the in-coupling event) the event's denominator cos(ic1) (kJBlockF32; block 0's
 // cosA_2 slot holds the growth bound, and a two-branch block never reads cosA_2).
-__device__ __forceinline__ double4 block_cw(const double *B, bool entry, double &growth, double &cos_ic1) {
+// Wsum's sign bit flags a block with a branch matrix that is not scaled-unitary (amp_blk: the
+// amplification step runs there; wgrt_pack.h).
+__device__ __forceinline__ double4 block_cw(const double *B, bool entry, double &growth, double &cos_ic1,
+                                            bool &amp_blk) {
     const double2 c01 = *(const double2 *)(B + kJBlockCos);
     const float4 fw = *(const float4 *)(B + kJBlockF32);
     growth = (double)(entry ? fw.y : fw.z);
     cos_ic1 = __hiloint2double(__float_as_int(fw.w), __float_as_int(fw.z));
-    return double4{c01.x, c01.y, (double)fw.y, (double)fw.x};
+    amp_blk = __float_as_uint(fw.x) >> 31;
+    return double4{c01.x, c01.y, (double)fw.y, (double)fabsf(fw.x)};
 }
 
 // The efficiencies from the single-precision Hermitian forms (the estimate every decision starts
@@ -946,6 +950,52 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
     d.a2 = three ? q[2] * B[kJBlockCos2] * inv * inv_n_g : 0.0;
 }
 
+// Amplification of the lanes' state discrepancy (DESIGN.md §2.4, "The bound, stated").  Both lanes apply
+// the same Jones matrix M to states that differ, up to a global phase, by a chordal distance eps; after the
+// normalisation the distance is at most a eps / (1 - eps / rho) (first order exact: a = |det M| |E|^2 /
+// |M E|^2, the stretch of the direction orthogonal to E over that of E; rho = |M E| / (sigma_max |E|)).
+// For a scaled-unitary M, a = 1; a singular one contracts (a = 0); a = kappa at worst, for the least
+// transmitted polarisation -- the branch the Monte-Carlo draw takes least often.  The Jones lane carries
+// A = prod max(1, a_k) (JRay::amp, times 1.006 per step for the second-order term and this evaluation's
+// rounding) and scales its certification bound by it; a branch with rho < 1e3 x the discrepancy bound is
+// abandoned (kUncertain).  The step runs only in blocks whose branch matrices are not scaled-unitary to
+// within kappa^2 <= 1 + 1e-6 (the sign bit of the block's float Wsum, wgrt_pack.h): a unitary branch has
+// a <= kappa <= 1 + 5e-7 for every state, so those blocks' factors multiply to at most exp(5e-7 n), 1.05
+// at the 1e5-bounce cap, which the bound's margin covers (§2.4).  WGRT_AMPLIFY=0 builds without it (the
+// round-5 bound, proven for scaled-unitary matrices only).
+#ifndef WGRT_AMPLIFY
+#define WGRT_AMPLIFY 1
+#endif
+constexpr bool kAmplify = WGRT_AMPLIFY != 0;
+
+// |det M|^2 = det H, bounded from above from the tile's single-precision H = M^H M: the float products
+// are exact in double and the float entries carry 2^-24 relative rounding, so det H lies within
+// 7 2^-24 h11 h22 of this evaluation (|h12|^2 <= h11 h22).
+__device__ __forceinline__ double det2_ub(const float4 &h) {
+    const double hx = h.x, hy = h.y, hz = h.z, hw = h.w;
+    const double d = hx * hy - (hz * hz + hw * hw);
+    return fmax(d, 0.0) + 0x1p-21 * (hx * hy);
+}
+
+// The decision's half of a taken branch's amplification step, from the branch's H (single precision),
+// e2 = |E|^2 and q = the discrepancy bound the decision used (cert_tol (1 + G (n / 100)^2) amp):
+// pa = |det M|^2 |E|^4 (so a^2 = pa / |M E|^4), and nmin = 1e6 q^2 trace(H) |E|^2, the least |M E|^2 with
+// rho >= 1e3 q (sigma_max^2 <= trace H); both rounded up into floats.
+__device__ __forceinline__ void amp_prepare(const float4 &hb, double e2, double q, float &pa, float &nmin) {
+    pa = (float)(det2_ub(hb) * e2 * e2 * (1.0 + 0x1p-20));
+    nmin = (float)(1e6 * q * q * ((double)hb.x + (double)hb.y) * e2 * (1.0 + 0x1p-20));
+}
+
+// The take's half: amp times max(1, a) (rn = 1 / |M E| to ~1 ulp), or a negative value when |M E|^2 = n2
+// is below nmin (the first-order step is not certain there: the ray is abandoned).
+__device__ __forceinline__ float amp_step(float amp, float pa, float nmin, double n2, double rn) {
+    const double r2 = rn * rn;
+    const double a2 = (double)pa * r2 * r2;
+    float out = amp;
+    if (__builtin_expect(a2 > 1.0, 0)) out = (float)((double)amp * sqrt(a2) * 1.006);
+    return n2 < (double)nmin ? -1.0f : out;
+}
+
 // Same contract as interact() (GRTF:860-904 and the branch bodies of GRTF:905-1246), plus
 // kUncertain: the decision could not be certified; the lane's ray must be abandoned (nothing
 // of it has been written) and replayed.
@@ -971,7 +1021,8 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const int ga = kind >= 3 ? 2 : 0;
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
     double growth, cos_ic1;
-    const double4 cw = block_cw(B, entry, growth, cos_ic1);
+    bool amp_blk;
+    const double4 cw = block_cw(B, entry, growth, cos_ic1, amp_blk);
     // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
     // issued together with its matrix, one memory round trip per interaction less
     const double2 mva = *(const double2 *)(T + kJGap + ga);
@@ -982,7 +1033,8 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double base = fma(nb * nb, growth, 1.0) * fabs(inv) * fmax(e2, 1.0);
+    const double grow = kAmplify ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
+    const double base = grow * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
@@ -1020,6 +1072,16 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
     const double rn = rsq_nr(n2);
+    if (kAmplify && __builtin_expect(amp_blk, 0)) {
+        // a non-unitary branch matrix: the amplification step (its inputs re-read here, off the common path)
+        const float4 hb = ((const float4 *)(B + kJBlockHerm))[b];
+        const double e2b = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
+        float pa, nmin;
+        amp_prepare(hb, e2b, A.cert_tol * grow, pa, nmin);
+        const float a = amp_step(r.amp, pa, nmin, n2, rn);
+        if (a < 0.0f) return kUncertain;
+        r.amp = a;
+    }
     r.er = f.er * rn;
     r.ei = f.ei * rn;
     r.mr = f.mr * rn;
@@ -1032,167 +1094,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     r.cos_t = ba ? cw.x : cw.y;
     r.gx = mv.x;
     r.gy = mv.y;
-    r.hr = hop.x;
-    r.hi = hop.y;
-    SEG_IMARK_DEP(sg, 5, r.er + r.ei + r.mr + r.mi + r.ener);
-    if (kind == 0) {
-        const bool in_ic = in_poly_w(loc, (typename Loc::Word)L.pf, kPolyIC, r.x, r.y, &K);
-        if (ba) return in_ic ? 0 : 2;
-        return in_ic ? 1 : kDie;
-    }
-    if (kind <= 2) return ba ? 2 : 3;
-    return ba ? 4 : 5;
-}
-
-// The same interaction in two halves, so that the wave issues ONE cell-word gather per pass for all
-// its lanes, between them (jones_body, WGRT_UNIFIED_CELL): interact_decide loads the block's line 0,
-// decides and moves the ray for a taken branch; the caller then loads the cell word of every lane that
-// moved (taken branches and miss hops) in one instruction; interact_take loads the taken matrix and hop
-// phasor and updates the field.  Each memory wait of a pass then covers every load the pass has in
-// flight: the line-0 wait the stores before it, the matrix wait every lane's new cell word -- where a
-// miss hop's gather issued in advance() used to hold up the line-0 wait of the lanes at an interaction
-// (vmcnt counts in issue order), and the next pass's advance() the stores of the out-coupling queue.
-// Amplification of the lanes' state discrepancy (DESIGN.md §2.4, "The bound, stated").  Both lanes apply
-// the same Jones matrix M to states that differ, up to a global phase, by a chordal distance eps; after the
-// normalisation the distance is at most a eps / (1 - eps / rho) (first order exact: a = |det M| |E|^2 /
-// |M E|^2, the stretch of the direction orthogonal to E over that of E; rho = |M E| / (sigma_max |E|)).
-// For a scaled-unitary M, a = 1; a singular one contracts (a = 0); a = kappa at worst, for the least
-// transmitted polarisation -- the branch the Monte-Carlo draw takes least often.  The Jones lane carries
-// A = prod max(1, a_k) (JRay::amp, times 1.006 per step for the second-order term and this evaluation's
-// rounding) and scales its certification bound by it; a branch with rho < 1e3 x the discrepancy bound is
-// abandoned (kUncertain).  WGRT_AMPLIFY=0 builds without it (the bound is then proven for
-// scaled-unitary matrices only, round 5).
-#ifndef WGRT_AMPLIFY
-#define WGRT_AMPLIFY 0
-#endif
-constexpr bool kAmplify = WGRT_AMPLIFY != 0;
-
-// |det M|^2 = det H, bounded from above from the tile's single-precision H = M^H M: the float products
-// are exact in double and the float entries carry 2^-24 relative rounding, so det H lies within
-// 7 2^-24 h11 h22 of this evaluation (|h12|^2 <= h11 h22).
-__device__ __forceinline__ double det2_ub(const float4 &h) {
-    const double hx = h.x, hy = h.y, hz = h.z, hw = h.w;
-    const double d = hx * hy - (hz * hz + hw * hw);
-    return fmax(d, 0.0) + 0x1p-21 * (hx * hy);
-}
-
-// The decision's half of a taken branch's amplification step, from the branch's H (single precision),
-// e2 = |E|^2 and q = the discrepancy bound the decision used (cert_tol (1 + G (n / 100)^2) amp):
-// pa = |det M|^2 |E|^4 (so a^2 = pa / |M E|^4), and nmin = 1e6 q^2 trace(H) |E|^2, the least |M E|^2 with
-// rho >= 1e3 q (sigma_max^2 <= trace H); both rounded up into floats.
-__device__ __forceinline__ void amp_prepare(const float4 &hb, double e2, double q, float &pa, float &nmin) {
-    pa = (float)(det2_ub(hb) * e2 * e2 * (1.0 + 0x1p-20));
-    nmin = (float)(1e6 * q * q * ((double)hb.x + (double)hb.y) * e2 * (1.0 + 0x1p-20));
-}
-
-// The take's half: amp times max(1, a) (rn = 1 / |M E| to ~1 ulp), or a negative value when |M E|^2 = n2
-// is below nmin (the first-order step is not certain there: the ray is abandoned).
-__device__ __forceinline__ float amp_step(float amp, float pa, float nmin, double n2, double rn) {
-    const double r2 = rn * rn;
-    const double a2 = (double)pa * r2 * r2;
-    float out = amp;
-    if (__builtin_expect(a2 > 1.0, 0)) out = (float)((double)amp * sqrt(a2) * 1.006);
-    return n2 < (double)nmin ? -1.0f : out;
-}
-
-struct JTake {
-    double cos_b;  // cosA_b: the next cos(theta)
-    double inv;    // 1 / cos(theta) (the taken branch's efficiency is n2 * cos_b * inv * f01, in that order)
-    double f01;    // n_g for the in-coupling event, else 1
-    double wb;     // SINGLE: the eerr increment's bound scale cert_tol * base * W[b] * 1.01
-    double2 hop;   // the new region's miss-hop phase step (loaded here, ahead of the caller's stores)
-    float pa;      // kAmplify: amp_prepare's |det M_b|^2 |E|^4 and least |M_b E|^2
-    float nmin;
-    bool ba;       // branch a (index 0) taken
-};
-
-template <bool SINGLE, class Loc>
-__device__ __forceinline__ int interact_decide(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
-                                               int kind, bool entry, JTake &tk, SegAcc *sg = nullptr) {
-    JRay &r = L.r;
-    const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
-    const double *B = T + kJHeader + kJBlock * blk;
-    const bool three = kind >= 3;
-    const bool thr = kind >= 1;
-    const double t = SINGLE ? A.threshold : 0.0;
-    const int ga = kind >= 3 ? 2 : 0;
-    const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
-    double growth, cos_ic1;
-    const double4 cw = block_cw(B, entry, growth, cos_ic1);
-    const double2 mva = *(const double2 *)(T + kJGap + ga);
-    const double2 mvb = *(const double2 *)(T + kJGap + gb);
-    const double denom = entry ? cos_ic1 : r.cos_t;
-    const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
-    const double inv = rcp_nr(denom);
-    const double f01 = entry ? A.n_g : 1.0;
-    const double nb = (double)L.bounces * 0.01;
-    const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double grow = kAmplify ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
-    const double base = grow * fabs(inv) * fmax(e2, 1.0);
-    JDecision d;
-    float4 h01[2];
-    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg, kAmplify ? h01 : nullptr);
-    jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
-    if (__builtin_expect(!d.ok, 0)) {
-        estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
-        jones_decide(d, u, A.cert_tol * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
-    }
-    SEG_IMARK_DEP(sg, 3, d.a0 + d.a1 + d.a2 + (d.ok ? 1.0 : 0.0) + (d.s0 ? 2.0 : 0.0) + (d.s1 ? 4.0 : 0.0));
-    const int code = !d.ok ? kUncertain : d.s2 ? kOut : !(d.s0 | d.s1) ? kDie : 0;
-    const bool ba = d.s0;
-    if (kAmplify) amp_prepare(ba ? h01[0] : h01[1], e2, A.cert_tol * grow, tk.pa, tk.nmin);
-    const double2 mv = ba ? mva : mvb;
-    tk.ba = ba;
-    tk.cos_b = ba ? cw.x : cw.y;
-    tk.inv = inv;
-    tk.f01 = f01;
-    tk.wb = SINGLE ? A.cert_tol * base * B[kJBlockW + (ba ? 0 : 1)] * 1.01 : 0.0;
-    if (code == 0) {   // the taken branch's new position (its cell word: the caller's gather)
-        r.x = r.x + mv.x;
-        r.y = r.y + mv.y;
-        r.gx = mv.x;
-        r.gy = mv.y;
-        // issued here, before the caller's queue and retire stores, so neither the compiler nor the
-        // in-order wait puts it behind the matrix (it is read by the next pass's miss hop)
-        tk.hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
-    }
-    return code;
-}
-
-// The taken branch's second half (after the caller's gather of L.pf at the new position): the field,
-// ener, the next region.  kUncertain for a field too small to normalise.
-template <bool SINGLE, class Loc>
-__device__ __forceinline__ int interact_take(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
-                                             int kind, const JTake &tk, SegAcc *sg = nullptr) {
-    JRay &r = L.r;
-    const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
-    const double *B = T + kJHeader + kJBlock * blk;
-    const bool ba = tk.ba;
-    const double2 hop = tk.hop;
-#ifdef WGRT_SEG
-    const Rec rec_b = load_rec(B + kJBlockRec + (ba ? 0 : 8));
-    SEG_IWAITVM(sg);
-    SEG_IMARK_DEP(sg, 4, rec_b.pr + rec_b.si + hop.x);
-    const JField f = jones(rec_b, r);
-#else
-    const JField f = jones(load_rec(B + kJBlockRec + (ba ? 0 : 8)), r);
-#endif
-    const double n2 = norm2(f);
-    if (!(n2 > 1e-300)) return kUncertain;
-    const double rn = rsq_nr(n2);
-    if (kAmplify) {
-        const float a = amp_step(r.amp, tk.pa, tk.nmin, n2, rn);
-        if (__builtin_expect(a < 0.0f, 0)) return kUncertain;
-        r.amp = a;
-    }
-    r.er = f.er * rn;
-    r.ei = f.ei * rn;
-    r.mr = f.mr * rn;
-    r.mi = f.mi * rn;
-    const double ab = n2 * tk.cos_b * tk.inv * tk.f01;   // interact()'s association
-    if (SINGLE) r.eerr += tk.wb * rcp_nr(ab) + 1e-15;
-    r.ener = r.ener * ab;
-    r.cos_t = tk.cos_b;
     r.hr = hop.x;
     r.hi = hop.y;
     SEG_IMARK_DEP(sg, 5, r.er + r.ei + r.mr + r.mi + r.ener);
@@ -1241,11 +1142,8 @@ __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); 
 // evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
-// UNI (WGRT_UNIFIED_CELL): a miss hop does not load its cell word here; it sets `reload` and the caller's
-// one gather per pass loads it (with the taken branches' cell words, after the decisions).
-template <bool UNI = false, class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind,
-                                       bool *reload = nullptr) {
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
@@ -1294,9 +1192,8 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
         const double mr = r.mr;
         r.mr = fma(mr, r.hr, -r.mi * r.hi);
         r.mi = fma(mr, r.hi, r.mi * r.hr);
-        if (!UNI) L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
+        L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
     }
-    if (UNI) *reload = hop;
     const int step = hit ? blkbase + sl : kTransit;
     const int next = ic ? 1 + region : step;
     return die ? kDie : next;

@@ -174,6 +174,7 @@ WGRT_HD void pack_tile(const PackView &v, int64_t g, double *T, double *J) {
         // states) TIR[0] / TIR[2], FC blocks TIR[0] / TIR[1], OC blocks TIR[1] / TIR[3]
         const int ta = b < 3 ? 0 : (three ? 1 : 0), tb = b < 3 ? 2 : (three ? 3 : 1);
         double sum = 0.0;
+        bool nonunitary = false;   // a taken branch (k < 2) whose matrix is not scaled-unitary
         O[kJBlockCos] = Bt[kBlockCos];
         O[kJBlockCos + 1] = Bt[kBlockCos + 1];
         O[kJBlockCos2] = Bt[kBlockCos + 2];
@@ -209,8 +210,18 @@ WGRT_HD void pack_tile(const PackView &v, int64_t g, double *T, double *J) {
             h[1] = (float)((rr * rr + ri * ri) + (sr * sr + si * si));
             h[2] = (float)((pr * rr + pi * ri) + (qr * sr + qi * si));   // Re(conj(p) r + conj(q) s)
             h[3] = (float)((pr * ri - pi * rr) + (qr * si - qi * sr));   // Im(conj(p) r + conj(q) s)
+            if (k < 2) {
+                // kappa^2 = s1^2 / s2^2 of H (s1^2 - s2^2 = sqrt((h11 - h22)^2 + 4 |h12|^2), no cancellation):
+                // not scaled-unitary once kappa^2 > 1 + 1e-6 (the Jones lane's amplification step, wgrt_device.h)
+                const double h11 = (pr * pr + pi * pi) + (qr * qr + qi * qi), h22 = (rr * rr + ri * ri) + (sr * sr + si * si);
+                const double g_re = (pr * rr + pi * ri) + (qr * sr + qi * si), g_im = (pr * ri - pi * rr) + (qr * si - qi * sr);
+                const double dif = sqrt((h11 - h22) * (h11 - h22) + 4.0 * (g_re * g_re + g_im * g_im));
+                const double s2 = 0.5 * ((h11 + h22) - dif);
+                if (h11 + h22 > 0.0 && !(dif <= 1e-6 * s2)) nonunitary = true;
+            }
         }
         f32[0] = (float)(sum * 1.01);   // 1.01: covers this bound's own rounding to float
+        if (nonunitary) f32[0] = -f32[0];   // the sign bit flags the block (block_cw)
         // the phase-growth bound with the block's line-0 loads (it only ever scales a tolerance up, so
         // rounded up); block 0 also carries the in-coupling event's denominator cos(ic1) as the bits
         // of a double, in place of the cosA_2 it does not have

@@ -66,7 +66,7 @@ __device__ __forceinline__ void atomic_max_pos(double *p, double v) {
 // Per-lane accumulators, flushed once per lane at the end.
 struct ShadowAcc {
     uint64_t decisions = 0, uncertain = 0, flips = 0, bounces = 0, fallbacks = 0;
-    double max_ratio = 0.0, max_ratio32 = 0.0, max_ener = 0.0;
+    double max_ratio = 0.0, max_ratio32 = 0.0, max_ener = 0.0, max_amp = 1.0;
     double max_depth[kDepthBuckets] = {0, 0, 0, 0, 0, 0};
     uint64_t n_depth[kDepthBuckets] = {0, 0, 0, 0, 0, 0};
     uint64_t hist[kHistBuckets] = {};
@@ -113,6 +113,7 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
         jr.ei = 0.0;
         jr.mr = cd * Etm;
         jr.mi = sd * Etm;
+        jr.amp = 1.0f;
     }
     double jener = 1.0, eerr = 0.0;
     uint32_t hops = 0;
@@ -152,13 +153,15 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
             }
             hops = 0;
             double growth, cos_ic1;
-            const double4 cw = block_cw(JB, entry, growth, cos_ic1);
+            bool amp_blk;
+            const double4 cw = block_cw(JB, entry, growth, cos_ic1, amp_blk);
             const double jden = entry ? cos_ic1 : cos_th;
             const double inv = rcp_nr(jden);
             const double f01 = entry ? A.n_g : 1.0;
             const double nb = (double)bounces * 0.01;
             const double en2 = fma(jr.er, jr.er, fma(jr.ei, jr.ei, fma(jr.mr, jr.mr, jr.mi * jr.mi)));
-            const double base = fma(nb * nb, growth, 1.0) * fabs(inv) * fmax(en2, 1.0);
+            const double grow = kAmplify ? fma(nb * nb, growth, 1.0) * (double)jr.amp : fma(nb * nb, growth, 1.0);
+            const double base = grow * fabs(inv) * fmax(en2, 1.0);
             const double c_ref[3] = {e0, e0 + e1, e0 + e1 + e2};
             // how much of each bound the arithmetic uses against the reference's thresholds
             auto ratio = [&](const JDecision &d, double scl) {
@@ -197,6 +200,15 @@ __device__ void shadow_trace(const TraceArgs &A, const Loc &loc, int64_t i, Shad
                 const JField f = jones(load_rec(JB + kJBlockRec + 8 * b), jr);
                 const double n2 = norm2(f);
                 const double rn = rsq_nr(n2);
+                if (kAmplify && amp_blk) {   // the product lane's amplification step (wgrt_device.h interact)
+                    const float4 hb = ((const float4 *)(JB + kJBlockHerm))[b];
+                    float pa, nmin;
+                    amp_prepare(hb, en2, A.cert_tol * grow, pa, nmin);
+                    const float a = amp_step(jr.amp, pa, nmin, n2, rn);
+                    if (a < 0.0f) ++acc.uncertain;   // the product lane abandons the ray here
+                    else jr.amp = a;
+                    acc.max_amp = fmax(acc.max_amp, (double)jr.amp);
+                }
                 jr.er = f.er * rn;
                 jr.ei = f.ei * rn;
                 jr.mr = f.mr * rn;
@@ -297,6 +309,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(ShadowArgs S, Loc loc) {
     const uint64_t dec = wave_sum(acc.decisions), unc = wave_sum(acc.uncertain), fl = wave_sum(acc.flips);
     const uint64_t bo = wave_sum(acc.bounces), fb = wave_sum(acc.fallbacks);
     const double mr = wave_max(acc.max_ratio), mr32 = wave_max(acc.max_ratio32), me = wave_max(acc.max_ener);
+    const double ma = wave_max(acc.max_amp);
     if (lead) {
         atomicAdd((unsigned long long *)&o->decisions, (unsigned long long)dec);
         atomicAdd((unsigned long long *)&o->uncertain, (unsigned long long)unc);
@@ -306,6 +319,7 @@ __global__ __launch_bounds__(256) void shadow_kernel(ShadowArgs S, Loc loc) {
         atomic_max_pos(&o->max_ratio, mr);
         atomic_max_pos(&o->max_ratio32, mr32);
         atomic_max_pos(&o->max_ener_ratio, me);
+        atomic_max_pos(&o->max_amp, ma);
     }
     for (int k = 0; k < kDepthBuckets; ++k) {
         const double v = wave_max(acc.max_depth[k]);

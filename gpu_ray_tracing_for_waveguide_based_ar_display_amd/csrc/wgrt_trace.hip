@@ -216,15 +216,6 @@ constexpr int64_t kStripe = WGRT_STRIPE;
 #define SEG_TMARK(sg, k, dep) ((void)0)
 #endif
 
-// One cell-word gather per pass for every lane that moved (taken branches and miss hops), issued after
-// the decisions (wgrt_device.h interact_decide / interact_take).
-#ifndef WGRT_UNIFIED_CELL
-#define WGRT_UNIFIED_CELL 0
-#endif
-constexpr bool kUnifiedCell = WGRT_UNIFIED_CELL != 0;
-#ifndef WGRT_LATE_RETIRE
-#define WGRT_LATE_RETIRE 1
-#endif
 #ifndef WGRT_ONE_RETIRE
 #define WGRT_ONE_RETIRE 1
 #endif
@@ -338,7 +329,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     // that ended in the previous pass's interaction and those advance() ends (fused launches retire at
     // once: their hand-off would wait a pass)
     constexpr bool ONE = !FUSED && kOneRetire;
-    constexpr bool UNI = kUnifiedCell;
     bool fin = false;
     const int lane = threadIdx.x & 63;
     const int64_t n_chunks = (A.n_rays + chunk - 1) / chunk;
@@ -366,7 +356,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     JLane L;
     int blk = 0, kind = 0;
     bool entry = false;
-    bool reload = false;   // UNI: this lane's miss hop moved it; its cell word is loaded in interact_pass
     // per-lane totals in 32 bits: a lane's bounce total is added to the stats directly before it
     // could overflow (2^31 bounces on one lane: never in practice)
     uint32_t tot_b = 0, tot_bad = 0, tot_giveup = 0, tot_int = 0;
@@ -549,53 +538,27 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         }
     };
 
-    // the second half of a pass: the interaction of the lanes at one, and this pass's out-couplings.
-    // UNI: decide, queue the out-couplings, load the new cell word of every lane that moved (taken
-    // branches and miss hops: one gather instruction), then the taken branches' matrices.
-    auto interact_pass = [&](SegAcc *sg, bool late_retire) {
+    // the second half of a pass: the interaction of the lanes at one, and this pass's out-couplings
+    auto interact_pass = [&](SegAcc *sg) {
         if (TL && tl_on) {
             ++tl_passes;
             tl_lanes += __popcll(__ballot(active));
         }
-        if (UNI) {
-            const bool inter = active && blk >= 0;
-            JTake tk;
-            int next = 0;
-            if (inter) {
-                L.inter += entry ? 0u : 1u;
-                next = interact_decide<SINGLE>(A, K, loc, L, blk, kind, entry, tk, sg);
-            }
-            SEG_TMARK(sg, 2, (double)next);
-            queue_out(inter && next == kOut);
-            if (late_retire && fin) {   // (launch tail: its stores go out behind the line-0 wait)
-                retire();
-                fin = false;
-            }
-            SEG_TMARK(sg, 3, 0.0);
-            const bool take = inter && next == 0;
-            if (take || (active && reload)) L.pf = locate_c(loc, L.r.x, L.r.y);   // read by the next pass
-            SEG_TMARK(sg, 4, 0.0);
-            if (take) next = interact_take<SINGLE>(A, K, loc, L, blk, kind, tk, sg);
-            SEG_TMARK(sg, 5, L.r.er + (double)next);
-            if (inter) outcome(next);
-        } else {
-            bool out = false;
-            if (active && blk >= 0) {
-                L.inter += entry ? 0u : 1u;
-                const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
-                out = next == kOut;
-                outcome(next);
-            }
-            SEG_TMARK(sg, 5, L.r.er);
-            queue_out(out);
+        bool out = false;
+        if (active && blk >= 0) {
+            L.inter += entry ? 0u : 1u;
+            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
+            out = next == kOut;
+            outcome(next);
         }
+        SEG_TMARK(sg, 5, L.r.er);
+        queue_out(out);
         SEG_MARK(sg, 6);
     };
 
     for (;;) {
-        reload = false;
         if (active) {
-            blk = advance<UNI>(A, K, loc, L, kind, &reload);
+            blk = advance(A, K, loc, L, kind);
             entry = false;
             if (ONE) fin |= blk == kDie;
             else if (blk == kDie) retire();
@@ -714,7 +677,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
         // the tail loop below
         if (!FUSED && exhausted) break;
-        interact_pass(nullptr, false);
+        interact_pass(nullptr);
     }
     if (!FUSED && __ballot(active) != 0ull) {
         // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
@@ -731,9 +694,6 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 #else
         SegAcc *const sg = nullptr;
 #endif
-        // UNI single launches retire the rays that ended inside interact_pass, after the line-0 loads, so
-        // that the retire stores do not hold up the line-0 wait (vmcnt counts stores in issue order)
-        constexpr bool LATE = ONE && UNI && WGRT_LATE_RETIRE;
         for (bool first = true;; first = false) {
 #ifdef WGRT_SEG
             if (sg) {
@@ -741,16 +701,14 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
                 if (seg_first_lane()) seg.p[8] = t0;
             }
 #endif
-            // (the first pass continues the main loop's: its miss hops' reload flags stand)
-            if (!first) reload = false;
             if (!first && active) {
-                blk = advance<UNI>(A, K, loc, L, kind, &reload);
+                blk = advance(A, K, loc, L, kind);
                 entry = false;
                 if (ONE) fin |= blk == kDie;
                 else if (blk == kDie) retire();
             }
             SEG_MARK_DEP(sg, 0, (double)blk + L.r.x);
-            if (ONE && !LATE && fin) {
+            if (ONE && fin) {
                 retire();
                 fin = false;
             }
@@ -759,11 +717,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 #ifdef WGRT_SEG
             if (seg_first_lane()) seg.p[7] += 1u;
 #endif
-            interact_pass(sg, LATE);
-        }
-        if (LATE && fin) {   // ended in the last pass's interaction
-            retire();
-            fin = false;
+            interact_pass(sg);
         }
 #ifdef WGRT_SEG
         // segment sums: words 8..15 of a 16-word wave record (tools/segments.py)

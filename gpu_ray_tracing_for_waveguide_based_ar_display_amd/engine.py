@@ -353,7 +353,7 @@ def shadow(scene: Scene, rays: dict, rng_states: torch.Tensor, gid_offset: int =
             "max_ratio32_by_depth": dict(zip(SHADOW_DEPTHS, list(st.max_ratio_by_depth))),
             "decisions_by_depth": dict(zip(SHADOW_DEPTHS, [int(v) for v in st.decisions_by_depth])),
             "ratio32_hist_log10": {f"1e{b - 18}": int(v) for b, v in enumerate(st.ratio_hist) if v},
-            "max_ener_ratio": st.max_ener_ratio}
+            "max_ener_ratio": st.max_ener_ratio, "max_amp": st.max_amp}
 
 
 def selftest_math(a: torch.Tensor, b: torch.Tensor, stream=None) -> torch.Tensor:

@@ -81,6 +81,11 @@ PROFILES = {
     "adversarial_singular": dict(ic=(0.40, 0.05), r0=(0.85, 0.05), r1=(0.05, 0.85),
                                  fc_fold=(0.08, 0.30), fc_keep=0.97, fc_back=0.04, fc2_keep=0.93,
                                  oc_turn=0.03, oc_out=(0.06, 0.25), oc_keep=0.96, jones="singular", cond=1e6),
+    # * rank-one Jones matrices plus 1e-9 of a unitary one (condition ~1e9): the taken branch contracts the
+    #   state's polarisation onto one direction, and the least-transmitted one is ~1e-18 of the most;
+    "adversarial_rank1": dict(ic=(0.40, 0.05), r0=(0.85, 0.05), r1=(0.05, 0.85),
+                              fc_fold=(0.08, 0.30), fc_keep=0.97, fc_back=0.04, fc2_keep=0.93,
+                              oc_turn=0.03, oc_out=(0.06, 0.25), oc_keep=0.96, jones="singular", cond=1e9),
     # * lossless interactions whose branch efficiencies sum to 1 - 1e-9 and split (nearly) evenly, no
     #   jitter: every interaction's last threshold sits 1e-9 below 1 (draws near 1 decide against it)
     #   and the branch thresholds sit near the common draw 0.5; with shortened hops (tests scale

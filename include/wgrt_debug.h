@@ -68,6 +68,8 @@ typedef struct {
     uint64_t ratio_hist[20];     /* decisions by log10 of their ratio32: bucket b = [1e(b-18),
                                     1e(b-17)); bucket 0 also holds smaller ratios, 19 larger ones    */
     double max_ener_ratio;       /* single wavelength: max |ener_jones / ener_ref - 1| / tracked bound */
+    double max_amp;              /* the largest amplification bound a Jones lane carried (JRay::amp; 1 on
+                                    scaled-unitary LUTs) */
 } wgrt_shadow_stats;
 
 wgrt_status wgrt_debug_shadow(const wgrt_scene *scene, const wgrt_rays *rays, int64_t n_rays, int64_t gid_offset,

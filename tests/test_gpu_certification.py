@@ -111,6 +111,13 @@ def test_shadow_follows_reference(dev):
                                gap_scale=0.05, tir_near_pi=True)),
     ("adv_singular_single_guard", dict(nx=7, ny=7, lambdas=[2], R=4096, profile="adversarial_singular",
                                        gap_scale=0.25, wavelength=2)),
+    # rank-one matrices + 1e-9 of a unitary one (condition ~1e9), where the amplification-tracked bound
+    # (round 6, wgrt_device.h amp_step) is what makes the certification provable
+    ("adv_rank1_C3", dict(nx=21, ny=21, lambdas=[0, 1, 2], R=1024, profile="adversarial_rank1")),
+    ("adv_rank1_deep", dict(nx=11, ny=11, lambdas=[0, 1, 2], R=4096, profile="adversarial_rank1",
+                            gap_scale=0.05, tir_near_pi=True)),
+    ("adv_rank1_single_guard", dict(nx=7, ny=7, lambdas=[2], R=4096, profile="adversarial_rank1",
+                                    gap_scale=0.25, wavelength=2)),
 ])
 def test_certification_slack(dev, name, cfg):
     st, *_ = _shadow_run(dev, **cfg)
@@ -118,6 +125,8 @@ def test_certification_slack(dev, name, cfg):
     print(name, json.dumps(st))
     assert st["decisions"] > 0
     assert st["silent_flips"] == 0
+    if not name.startswith("adv_"):
+        assert st["max_amp"] <= 1.0, st   # scaled-unitary LUTs: the amplification step never runs
     assert st["max_ratio"] <= 1e-2, st      # double-precision evaluation vs its bound
     assert st["max_ratio32"] <= 0.5, st     # single-precision estimate vs its bound
     # the double-precision re-evaluation is correct, only slower; the lossless long-phase profile's rays
@@ -143,6 +152,9 @@ def test_certification_slack(dev, name, cfg):
                                gap_scale=0.05, tir_near_pi=True)),
     ("adv_lossless_long", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_lossless",
                                gap_scale=0.05, tir_near_pi=True)),
+    ("adv_rank1", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_rank1")),
+    ("adv_rank1_deep", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_rank1",
+                            gap_scale=0.05, tir_near_pi=True)),
 ])
 @pytest.mark.parametrize("variant", [7, 9, 1])
 def test_adversarial_luts_match_oracle(dev, name, cfg, variant):
