@@ -57,6 +57,7 @@ EMULATE_STEPS = 20              # single launches per shard in the emulated_stro
 # emulated_strong: BASELINE configs 3 and 4, and config 5 on the design geometry (C5d) and as the
 # short-hop stress batch (C5, fewer launches: 60 ms each on one GPU)
 EMULATE_CONFIGS = (("C3", EMULATE_STEPS), ("C4", EMULATE_STEPS), ("C5d", EMULATE_STEPS), ("C5", 4))
+FUSED_EMULATE = ("C3", "C4")    # emulated_strong also times the fused shape (the steps as one call) per shard
 # the strong-scaling gather's transfer, modelled: every rank sends its payload (1/N of the eyebox grid) to
 # rank 0 over its own xGMI link at the same time; one direction of a link carries half of the
 # ~153.6 GB/s per-link figure of the node, and one RCCL gather call adds a fixed cost
@@ -252,6 +253,7 @@ def main(argv=None):
             e_el, e_b, e_bl, e_ms = timed(steps, 0)
             extras[key] = {"value": round(e_b / e_el, 1), "ms_per_step": round(e_el / steps * 1e3, 4),
                            "steps": steps, "kernel_avg_ms": round(float(np.mean(e_ms)), 4), "note": note}
+        extras["region"] = region_cost(timed, call_ms, elapsed, _el, a.steps)
         if a.steps < LONG_STEPS:
             l_el, l_b, _, _ = timed(LONG_STEPS, 1, events=False)
             extras["long_region"] = {
@@ -297,7 +299,10 @@ def main(argv=None):
                 traffic_note = ("rocprofv3 PMC passes of the trace kernel on this build (tools/pmc_traffic.py): traffic "
                                 "= 2 x FETCH_SIZE + WRITE_SIZE per launch (the guide's gfx950 correction of FETCH_SIZE; "
                                 "L2 <-> fabric bytes, Infinity-Cache hits included, so an upper bound on HBM bytes), "
-                                "traffic_raw = FETCH_SIZE + WRITE_SIZE; measured_gbps = traffic / launch_avg_ms")
+                                "traffic_raw = FETCH_SIZE + WRITE_SIZE; measured_gbps = traffic / launch_avg_ms.  The x2 "
+                                "was calibrated in MI355X_MICROARCH.md on 16-B-per-lane streaming reads; this kernel's "
+                                "bytes are mostly 4-B cell-word gathers and 16-B tile reads, for which it is "
+                                "uncalibrated, so the true fabric traffic lies between traffic_raw and traffic")
         except (OSError, ValueError, KeyError):
             pass
         valu = pmc_roofline(a.pmc_json, f"{cname}:v{a.variant}", sha)
@@ -314,7 +319,8 @@ def main(argv=None):
                         "note": "no PMC summary recorded for this library build (tools/pmc_summary.py)"},
                     "binding": binding,
                     "note": "achieved = algorithmic bytes (72 B x bounces) / launch_avg_ms; launch_avg_ms: HIP events "
-                            "around each launch (trace kernel + the kernel behind it: replay_kernel, or epilogue_kernel for fused calls) on rank 0, in a "
+                            "around each launch (a single launch is the trace kernel alone since round 6: its replay "
+                            "runs inside it) on rank 0, in a "
                             "second pass of the same K launches (the timed steps carry no event records); valu: the "
                             "issue-side bound SURVEY.md §8(d) calls binding (VALU busy = SQ_ACTIVE_INST_VALU x 4 / "
                             "(GRBM_GUI_ACTIVE / 8 x 1024 SIMDs))"}
@@ -346,6 +352,7 @@ def main(argv=None):
             "main_job": extras.get("main_job"),
             "fused": extras.get("fused"),
             "long_region": extras.get("long_region"),
+            "region": extras.get("region"),
             "weak": extras.get("weak"),
             "emulated_strong": emulated,
             "cpu_baseline": cpu,
@@ -354,6 +361,28 @@ def main(argv=None):
     scene.close()
     if world > 1:
         dist.destroy_process_group()
+
+
+def region_cost(timed, call_ms, elapsed, ev_elapsed, steps):
+    """Where a short timed region's fixed cost goes: the region's wall time against
+    K x the per-launch time, for regions of 1, 5, 20 and 200 single launches (a least-squares line:
+    intercept = fixed cost per region, slope = per step), and inside the headline's evented pass the
+    first launch's HIP-event time against the median launch's (the first launch of a region starts on an
+    idle GPU after the barrier and synchronize)."""
+    ks, ts = [], []
+    for k in (1, 5, 20, 200):
+        el, _, _, _ = timed(k, 1, events=False)
+        ks.append(k)
+        ts.append(el * 1e3)
+    slope, icpt = np.polyfit(np.array(ks, float), np.array(ts, float), 1)
+    med = float(np.median(call_ms))
+    return {"regions_ms": {str(k): round(t, 4) for k, t in zip(ks, ts)},
+            "fixed_ms_per_region": round(float(icpt), 4), "ms_per_step_fit": round(float(slope), 4),
+            "first_launch_ms": round(float(call_ms[0]), 4), "median_launch_ms": round(med, 4),
+            "first_minus_median_ms": round(float(call_ms[0]) - med, 4),
+            "evented_wall_minus_launches_ms": round(ev_elapsed * 1e3 - float(np.sum(call_ms)), 4),
+            "note": f"the headline's {steps}-step region carries the fixed cost once; the fit's slope is the "
+                    "steady per-step time (the 200-step long_region's figure)"}
 
 
 def binding_record(scene, rays, rng, eb, shard, R, dev, lifetimes):
@@ -385,12 +414,13 @@ def binding_record(scene, rays, rng, eb, shard, R, dev, lifetimes):
                     "star's reporting roof, not the binding one"}
 
 
-def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="interleaved"):
+def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="interleaved", fused=False):
     """Each of the N strong-scaling shards of workload w (distributed.make_shard) traced alone on this
     GPU: ``steps`` single launches (HIP events around them) and 4-chained calls (the reference's
-    job shape, MAIN:169-177, one persistent launch; the median of five).  Returns the per-rank ms per step and the
-    predicted N-GPU step time = the slowest shard's (the eyebox collective not included: see
-    collective_cost)."""
+    job shape, MAIN:169-177, one persistent launch; the median of five); with ``fused``, also the bench's
+    ``fused`` shape: the ``steps`` chained traces as ONE call (one persistent launch; the median of three).
+    Returns the per-rank ms per step and the predicted N-GPU step time = the slowest shard's (the eyebox
+    collective not included: see collective_cost)."""
     import torch
 
     from gpu_ray_tracing_for_waveguide_based_ar_display_amd.distributed import (hip_shard_builder, hip_tracer,
@@ -413,7 +443,7 @@ def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="i
     for r in range(N):
         shard = make_shard(nx, ny, len(lambdas), R, N, r, assign)
         rays, rng = hip_shard_builder(points, nx, ny, lambdas, R, dev)(shard)
-        reserve(scene, shard.n_rays, 4)
+        reserve(scene, shard.n_rays, max(4, steps if fused else 0))
         run_steps(tracer, rays, rng, eb, shard.gid, warmup, 1)
         run_steps(tracer, rays, rng, eb, shard.gid, 4, 0)
         torch.cuda.synchronize()
@@ -426,17 +456,27 @@ def emulate_shards(scene, w, points, N, steps, warmup, dev, variant=0, assign="i
         job = float(np.median([ev_time(lambda: run_steps(tracer, rays, rng, eb, shard.gid, 4, 0)) / 4
                                for _ in range(5)]))
         check_stats(stats)
-        per_rank.append({"rank": r, "rays": shard.n_rays, "ms_per_step": round(ms, 4),
-                         "job_ms_per_step": round(job, 4), "bounces_per_step": b})
+        rec = {"rank": r, "rays": shard.n_rays, "ms_per_step": round(ms, 4), "job_ms_per_step": round(job, 4),
+               "bounces_per_step": b}
+        if fused:
+            run_steps(tracer, rays, rng, eb, shard.gid, steps, 0)
+            rec["fused_ms_per_step"] = round(float(np.median(
+                [ev_time(lambda: run_steps(tracer, rays, rng, eb, shard.gid, steps, 0)) / steps for _ in range(3)])), 4)
+            check_stats(stats)
+        per_rank.append(rec)
         del rays, rng
     worst = max(p["ms_per_step"] for p in per_rank)
     worst_job = max(p["job_ms_per_step"] for p in per_rank)
     total = sum(p["bounces_per_step"] for p in per_rank)
-    return {"steps": steps, "per_rank": per_rank, "predicted_ms_per_step": worst,
-            "predicted_value": round(total / (worst / 1e3), 1), "predicted_job_ms_per_step": worst_job,
-            "predicted_job_value": round(total / (worst_job / 1e3), 1),
-            "note": "each rank's shard timed alone on one MI355X; predicted N-GPU step = max over ranks, "
-                    "without the eyebox collective"}
+    out = {"steps": steps, "per_rank": per_rank, "predicted_ms_per_step": worst,
+           "predicted_value": round(total / (worst / 1e3), 1), "predicted_job_ms_per_step": worst_job,
+           "predicted_job_value": round(total / (worst_job / 1e3), 1),
+           "note": "each rank's shard timed alone on one MI355X; predicted N-GPU step = max over ranks, "
+                   "without the eyebox collective"}
+    if fused:
+        worst_f = max(p["fused_ms_per_step"] for p in per_rank)
+        out.update(predicted_fused_ms_per_step=worst_f, predicted_fused_value=round(total / (worst_f / 1e3), 1))
+    return out
 
 
 def collective_cost(scene, w, N, dev, assign="interleaved", reps=10):
@@ -498,11 +538,15 @@ def emulated_strong(a, scene, dev):
         w = CONFIGS[cname]
         geom, luts, points = build_inputs(w, lut_seed=a.lut_seed)
         sc = scene if cname == "C3" else Scene.from_geometry(geom, luts, device=dev.index or 0)
-        whole = emulate_shards(sc, w, points, 1, steps, 2, dev, a.variant, a.assign)
+        fused = cname in FUSED_EMULATE
+        whole = emulate_shards(sc, w, points, 1, steps, 2, dev, a.variant, a.assign, fused=fused)
         one, one_job = whole["predicted_ms_per_step"], whole["predicted_job_ms_per_step"]
         rec = {"one_gpu_ms_per_step": round(one, 4), "one_gpu_job_ms_per_step": one_job, "steps": steps}
+        if fused:
+            one_f = whole["predicted_fused_ms_per_step"]
+            rec["one_gpu_fused_ms_per_step"] = one_f
         for n in (2, 4, 8):
-            e = emulate_shards(sc, w, points, n, steps, 2, dev, a.variant, a.assign)
+            e = emulate_shards(sc, w, points, n, steps, 2, dev, a.variant, a.assign, fused=fused)
             c = collective_cost(sc, w, n, dev, a.assign)
             ms, job = e["predicted_ms_per_step"], e["predicted_job_ms_per_step"]
             ms_c, job_c = ms + c["total_ms"] / K, job + c["total_ms"] / 4
@@ -512,6 +556,13 @@ def emulated_strong(a, scene, dev):
                            "with_collective": {"ms_per_step": round(ms_c, 4), "speedup": round(one / ms_c, 3),
                                                "job_ms_per_step": round(job_c, 4),
                                                "job_speedup": round(one_job / job_c, 3)}}
+            if fused:
+                # the fused shape: the steps chained traces as one call per rank, the gather once per call
+                f = e["predicted_fused_ms_per_step"]
+                f_c = f + c["total_ms"] / steps
+                rec[str(n)].update(fused_ms_per_step=f, fused_speedup=round(one_f / f, 3))
+                rec[str(n)]["with_collective"].update(fused_ms_per_step=round(f_c, 4),
+                                                      fused_speedup=round(one_f / f_c, 3))
         if sc is not scene:
             sc.close()
         out[cname] = rec
@@ -519,9 +570,11 @@ def emulated_strong(a, scene, dev):
     out["note"] = ("strong scaling predicted on one MI355X: each of the N interleaved FoV x lambda shards "
                    "(bench.py --gpus N --scaling strong) traced alone, the slowest one's step time (HIP events, "
                    "the same method for the one-GPU baseline); single launches and the reference's 4-chained job "
-                   "per shard.  with_collective adds the eyebox gather: pack and rank-0 assembly timed on this "
-                   f"GPU, the transfer modelled at {XGMI_LINK_GBPS} GB/s per xGMI link plus {RCCL_CALL_MS} ms per "
-                   f"call; once per timed region of {K} steps for single launches, once per 4-trace job")
+                   "per shard, and for C3 / C4 the fused shape (the steps chained traces as one call per rank; "
+                   "fused_speedup against the one-GPU fused call timed the same way).  with_collective adds the "
+                   "eyebox gather: pack and rank-0 assembly timed on this GPU, the transfer modelled at "
+                   f"{XGMI_LINK_GBPS} GB/s per xGMI link plus {RCCL_CALL_MS} ms per call; once per timed region of "
+                   f"{K} steps for single launches, once per 4-trace job, once per fused call")
     return out
 
 
@@ -530,8 +583,8 @@ def kernel_name(variant, scene):
     when the scene has <= 16 polygons, else 9)."""
     if variant == 0:
         variant = 7 if scene.info()["n_polygons"] <= 16 else 9
-    return {1: "trace_grid_kernel", 7: "trace_jones_kernel<unsigned int, false, false>",
-            9: "trace_jones_kernel<unsigned long, false, false>"}[variant]
+    return {1: "trace_grid_kernel", 7: "trace_jones_kernel<unsigned int, false, false, false>",
+            9: "trace_jones_kernel<unsigned long, false, false, false>"}[variant]
 
 
 def cpu_baseline(geom, luts, points, nx, ny, lambdas, R, target_s):

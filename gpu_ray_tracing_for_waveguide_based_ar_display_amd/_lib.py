@@ -103,7 +103,7 @@ class SceneInfo(ctypes.Structure):
                 ("grid_cells_x", ctypes.c_int64), ("grid_cells_y", ctypes.c_int64),
                 ("grid_cell_mm", ctypes.c_double), ("grid_edge_cells", ctypes.c_int64),
                 ("n_polygons", ctypes.c_int32), ("device", ctypes.c_int32),
-                ("jtile_bytes", ctypes.c_int64)]
+                ("jtile_bytes", ctypes.c_int64), ("nonunitary_blocks", ctypes.c_int64)]
 
 
 _lib = None

@@ -961,8 +961,10 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
 // abandoned (kUncertain).  The step runs only in blocks whose branch matrices are not scaled-unitary to
 // within kappa^2 <= 1 + 1e-6 (the sign bit of the block's float Wsum, wgrt_pack.h): a unitary branch has
 // a <= kappa <= 1 + 5e-7 for every state, so those blocks' factors multiply to at most exp(5e-7 n), 1.05
-// at the 1e5-bounce cap, which the bound's margin covers (§2.4).  WGRT_AMPLIFY=0 builds without it (the
-// round-5 bound, proven for scaled-unitary matrices only).
+// at the 1e5-bounce cap, which the bound's margin covers (§2.4).  It lives in the AMP instantiations of
+// the trace kernel, which a launch runs when its scene has such a block (wgrt_scene::nonunitary_blocks):
+// on scaled-unitary LUTs the kernel carries none of it (compiled into every launch it cost 2-4 %).
+// WGRT_AMPLIFY=0 never selects them (the round-5 bound, proven for scaled-unitary matrices only).
 #ifndef WGRT_AMPLIFY
 #define WGRT_AMPLIFY 1
 #endif
@@ -1007,7 +1009,7 @@ __device__ __forceinline__ float amp_step(float amp, float pa, float nmin, doubl
 // abandoned.  The taken branch's field is always computed in double precision from its
 // double-precision matrix (loaded after the decision), so the carried Jones vector and ener
 // are the same values the all-double evaluation gives.
-template <bool SINGLE, class Loc>
+template <bool SINGLE, bool AMP, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
                                         int kind, bool entry, SegAcc *sg = nullptr) {
     JRay &r = L.r;
@@ -1033,7 +1035,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double f01 = entry ? A.n_g : 1.0;
     const double nb = (double)L.bounces * 0.01;
     const double e2 = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));
-    const double grow = kAmplify ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
+    const double grow = AMP ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
     const double base = grow * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
     estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg);
@@ -1072,7 +1074,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double n2 = norm2(f);
     if (!(n2 > 1e-300)) return kUncertain;
     const double rn = rsq_nr(n2);
-    if (kAmplify && __builtin_expect(amp_blk, 0)) {
+    if (AMP && __builtin_expect(amp_blk, 0)) {
         // a non-unitary branch matrix: the amplification step (its inputs re-read here, off the common path)
         const float4 hb = ((const float4 *)(B + kJBlockHerm))[b];
         const double e2b = fma(r.er, r.er, fma(r.ei, r.ei, fma(r.mr, r.mr, r.mi * r.mi)));

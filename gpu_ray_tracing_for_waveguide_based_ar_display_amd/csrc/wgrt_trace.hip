@@ -321,7 +321,7 @@ __device__ WGRT_REPLAY_INL void replay_tail(const KArgs &K, unsigned long long n
 // to n_iter launches: each ray's traces run in order from the same states; eyebox adds commute.
 // TL: the debug wave timeline (wgrt_debug_opts.timeline); the product instantiations have TL = false
 // and contain none of its code.
-template <bool FUSED, bool SINGLE, bool TL, class Loc>
+template <bool FUSED, bool SINGLE, bool TL, bool AMP, class Loc>
 __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, const Loc &loc, unsigned long long *heads,
                                           int chunk) {
     constexpr bool EPI = !FUSED && kInKernelEpilogue;
@@ -547,7 +547,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         bool out = false;
         if (active && blk >= 0) {
             L.inter += entry ? 0u : 1u;
-            const int next = interact<SINGLE>(A, K, loc, L, blk, kind, entry, sg);
+            const int next = interact<SINGLE, AMP>(A, K, loc, L, blk, kind, entry, sg);
             out = next == kOut;
             outcome(next);
         }
@@ -853,11 +853,13 @@ template <class CellT, bool FUSED, bool SINGLE>
 constexpr int jones_waves() {
     return (sizeof(CellT) == 4 && !FUSED && !SINGLE) ? WGRT_JONES_WAVES : 4;
 }
-template <class CellT, bool FUSED, bool SINGLE>
+// AMP: with the amplification step of the certification bound (wgrt_device.h; scenes with a block whose
+// branch matrices are not scaled-unitary)
+template <class CellT, bool FUSED, bool SINGLE, bool AMP>
 __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_kernel(TraceArgs A, LocatorT<CellT> loc,
                                                              unsigned long long *counter, int chunk) {
-    jones_body<FUSED, SINGLE, false>(A, kernel_kargs<decltype(trace_jones_kernel<CellT, FUSED, SINGLE>)>(), loc, counter,
-                                     chunk);
+    jones_body<FUSED, SINGLE, false, AMP>(
+        A, kernel_kargs<decltype(trace_jones_kernel<CellT, FUSED, SINGLE, AMP>)>(), loc, counter, chunk);
 }
 
 // The same loop with the debug wave timeline (wgrt_debug_opts.timeline; tools/timeline.py): a
@@ -865,8 +867,8 @@ __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void tr
 template <class CellT, bool FUSED, bool SINGLE>
 __global__ __launch_bounds__(256, (jones_waves<CellT, FUSED, SINGLE>())) void trace_jones_tl_kernel(
     TraceArgs A, LocatorT<CellT> loc, unsigned long long *counter, int chunk) {
-    jones_body<FUSED, SINGLE, true>(A, kernel_kargs<decltype(trace_jones_tl_kernel<CellT, FUSED, SINGLE>)>(), loc,
-                                    counter, chunk);
+    jones_body<FUSED, SINGLE, true, false>(A, kernel_kargs<decltype(trace_jones_tl_kernel<CellT, FUSED, SINGLE>)>(),
+                                           loc, counter, chunk);
 }
 
 __global__ __launch_bounds__(256) void classify_kernel(Locator L, int npoly, const double *xy, int64_t n,
@@ -1057,6 +1059,17 @@ __global__ __launch_bounds__(256) void classify_cells_kernel(const double *verts
 
 // One thread per (lambda, m, n) tile: the exact lane's tile and its Jones-vector tile
 // (wgrt_pack.h pack_tile, the host build's code); flags any non-finite value.
+// Blocks of the Jones tiles flagged non-scaled-unitary (the sign bit of their float Wsum, wgrt_pack.h):
+// counted once per scene, to pick the trace kernel instantiation (AMP) for its launches.
+__global__ __launch_bounds__(256) void nonunitary_kernel(const double *jtiles, int64_t ntiles, int jd, int nblk,
+                                                         unsigned long long *count) {
+    const int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= ntiles * nblk) return;
+    const int64_t g = i / nblk, b = i % nblk;
+    const float w = *(const float *)(jtiles + g * jd + kJHeader + kJBlock * b + kJBlockF32);
+    if (__float_as_uint(w) >> 31) atomicAdd(count, 1ull);
+}
+
 __global__ __launch_bounds__(64) void pack_tiles_kernel(PackView v, int64_t ntiles, double *tiles, double *jtiles,
                                                         int td, int jd, int *nonfinite) {
     const int64_t g = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -1238,6 +1251,23 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
         }
         s->edge_cells = (int64_t)ec;
     }
+    {   // the scene's non-scaled-unitary blocks (the trace kernel instantiation its launches run)
+        const int nblk = 3 + 2 * s->nfc + 2 * s->noc;
+        const int64_t nt = (int64_t)s->nl * s->nx * s->ny;
+        unsigned long long *cnt = nullptr;
+        HIP_TRY(hipMalloc((void **)&cnt, sizeof(unsigned long long)));
+        hipError_t e = hipMemset(cnt, 0, sizeof(unsigned long long));
+        if (e == hipSuccess && nt * nblk > 0) {
+            hipLaunchKernelGGL(nonunitary_kernel, dim3((unsigned)((nt * nblk + 255) / 256)), dim3(256), 0, 0, s->d_jtiles,
+                               nt, s->jtile_d, nblk, cnt);
+            e = hipGetLastError();
+        }
+        unsigned long long nu = 0;
+        if (e == hipSuccess) e = hipMemcpy(&nu, cnt, sizeof(nu), hipMemcpyDeviceToHost);
+        (void)hipFree(cnt);
+        if (e != hipSuccess) return bail(fail(WGRT_ERR_HIP, std::string("nonunitary_kernel: ") + hipGetErrorString(e)));
+        s->nonunitary_blocks = (int64_t)nu;
+    }
     {
         int cus = 0, per_cu = 0;
         HIP_TRY(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, device));
@@ -1247,8 +1277,13 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
             out = std::max(1, cus * std::max(1, per_cu));
             return e;
         };
-#define WGRT_GRID(CELL, C, F, S) \
-        HIP_TRY(grid_of((const void *)trace_jones_kernel<CELL, F, S>, s->jones_grid[C][F][S]))
+#define WGRT_GRID(CELL, C, F, S)                                                                              \
+        HIP_TRY(grid_of((const void *)trace_jones_kernel<CELL, F, S, false>, s->jones_grid[C][F][S]));        \
+        {   /* the AMP instantiation: the smaller of the two grids */                                        \
+            int g2 = 0;                                                                                       \
+            HIP_TRY(grid_of((const void *)trace_jones_kernel<CELL, F, S, true>, g2));                        \
+            s->jones_grid[C][F][S] = std::min(s->jones_grid[C][F][S], g2);                                   \
+        }
         WGRT_GRID(uint32_t, 0, false, false);
         WGRT_GRID(uint32_t, 0, false, true);
         WGRT_GRID(uint32_t, 0, true, false);
@@ -1309,6 +1344,7 @@ wgrt_status wgrt_scene_get_info(const wgrt_scene *s, wgrt_scene_info *info) {
     info->n_polygons = s->npoly;
     info->device = s->device;
     info->jtile_bytes = (int64_t)s->jtile_d * 8;
+    info->nonunitary_blocks = s->nonunitary_blocks;
     return WGRT_OK;
 }
 
@@ -1477,6 +1513,9 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     const bool timeline = dbg && dbg->timeline && dbg->timeline_waves > 0;
     if (timeline && (variant != 7 || single))
         return fail(WGRT_ERR_UNSUPPORTED, "the wave timeline is built for the full-colour 32-bit-cell kernel only");
+    if (timeline && kAmplify && s->nonunitary_blocks)
+        return fail(WGRT_ERR_UNSUPPORTED, "the wave timeline is built without the amplification step: scaled-unitary "
+                                          "LUTs only");
     if (num_iter > 1 && variant == 1) {   // chained launches, as the reference issues them
         LaunchCfg one = c;
         one.variant = variant;
@@ -1589,16 +1628,22 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     const int jchunk = A.order ? kChunk : ((dbg && dbg->chunk_rays > 0) ? std::min(dbg->chunk_rays, 64) : kChunk);
     const dim3 g3((unsigned)grid), b3(256);
     // instantiations: cell word width x fused chain x single-wavelength guard
-#define WGRT_LAUNCH_JONES(CELL, LOCV)                                                                              \
+#define WGRT_LAUNCH_JONES_A(CELL, LOCV, AMPV)                                                                      \
     do {                                                                                                           \
         if (num_iter > 1 && single)                                                                                \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, true>), g3, b3, 0, st, A, LOCV, ctr, jchunk);  \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, true, AMPV>), g3, b3, 0, st, A, LOCV, ctr, jchunk);  \
         else if (num_iter > 1)                                                                                     \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, false>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, true, false, AMPV>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
         else if (single)                                                                                           \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, true>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, true, AMPV>), g3, b3, 0, st, A, LOCV, ctr, jchunk); \
         else                                                                                                       \
-            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false>), g3, b3, 0, st, A, LOCV, ctr, jchunk);\
+            hipLaunchKernelGGL((trace_jones_kernel<CELL, false, false, AMPV>), g3, b3, 0, st, A, LOCV, ctr, jchunk);\
+    } while (0)
+    // the amplification step only for scenes that need it (wgrt_device.h kAmplify)
+#define WGRT_LAUNCH_JONES(CELL, LOCV)                                  \
+    do {                                                               \
+        if (kAmplify && s->nonunitary_blocks) WGRT_LAUNCH_JONES_A(CELL, LOCV, true);  \
+        else WGRT_LAUNCH_JONES_A(CELL, LOCV, false);                   \
     } while (0)
     if (timeline) {
         const LocatorT<uint32_t> l32 = make_locator32(s);
@@ -1613,6 +1658,7 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
         WGRT_LAUNCH_JONES(uint32_t, l32);
     }
 #undef WGRT_LAUNCH_JONES
+#undef WGRT_LAUNCH_JONES_A
     hipError_t e = hipGetLastError();
     if (e == hipSuccess && dbg && dbg->fail_after_trace) {
         mark_dirty(ms, sc);

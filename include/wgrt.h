@@ -130,6 +130,9 @@ typedef struct {
     int32_t n_polygons;
     int32_t device;
     int64_t jtile_bytes;       /* Jones-vector tile per (lambda, FoV) (variants 7 / 9)  */
+    int64_t nonunitary_blocks; /* ABI 7.  Interaction blocks whose taken branches' Jones matrices are not
+                                  scaled-unitary (kappa^2 > 1 + 1e-6): the Jones-vector variants then run
+                                  their amplification-tracked certification             */
 } wgrt_scene_info;
 
 /* Build the device-resident scene (packs LUT tiles, builds the exact polygon

@@ -96,5 +96,6 @@ def test_nonunitary_blocks_flagged(lib, profile, flagged):
         _, f = _w_mask(j.shape[1])
         wsum = np.ascontiguousarray(j[:, f]).view(np.float32)[:, 0::2]
         assert bool((wsum < 0).all()) if flagged else bool((wsum > 0).all()), (profile, int((wsum < 0).sum()), wsum.size)
+        assert sc.info()["nonunitary_blocks"] == int((wsum < 0).sum())   # ABI 7: the AMP kernels run iff > 0
     finally:
         sc.close()
