@@ -81,9 +81,6 @@ struct TraceArgs {
     // global ray ids of an interleaved shard (wgrt_launch_opts.gid_blocks): NULL = gid_offset + i
     const int64_t *gid_blocks;
     int64_t gid_block_rays;
-    // the launch tail's line-0 prefetch hints (wgrt_scene_build.h): the FC and OC slices as bands, the IC as a disc
-    SliceBands bfc, boc;
-    DiscHint icd;
 };
 
 constexpr int kPartWords = 8;   // counter partial slot of a trace workgroup (64-bit words)
@@ -629,7 +626,6 @@ struct JLane {
     uint32_t k;              // fused launches: the iteration (chained launch) this trace belongs to
     uint32_t s0;             // RNG state at the start of this trace (fused launches: replay point)
     uint64_t pf;             // locator cell word of (x, y), loaded a step ahead
-    int pb;                  // launch tail: the block whose line 0 this lane prefetched into LDS (-1: none)
 };
 
 enum : int { kUncertain = -3, kOut = -4 };
@@ -954,90 +950,6 @@ __device__ __forceinline__ void estimate64(JDecision &d, const double *B, const 
     d.a2 = three ? q[2] * B[kJBlockCos2] * inv * inv_n_g : 0.0;
 }
 
-// ---- the launch tail's line-0 prefetch (jones_body's tail loop: interact / advance with PF) ----
-// When a lane moves (a taken branch, a miss hop) or switches R3 -> R4, the block its next interaction will
-// use is predicted from the new position -- the coupler's slice from its band model, the in-coupler from
-// its disc (SliceBands / DiscHint) -- and that block's line 0 (the estimate's five 16-B pieces) and the
-// region's two branch moves are loaded straight into the lane's LDS slots (7 direct-to-LDS loads), in the
-// same instruction group as the new cell word.  The next interaction reads them from LDS when the cell
-// word confirms the prediction, so its decision no longer waits for a line-0 round trip -- which, with
-// vmcnt counting in issue order, also waited for every miss hop's cell word issued before it.
-// WGRT_TAIL_PREFETCH: 0 off, 1 on; diagnostics (tools/ab.py): 2 = predictions computed but nothing
-// prefetched (every interaction loads line 0 itself), 3 = that without the tail pass's vmcnt(0)
-#ifndef WGRT_TAIL_PREFETCH
-#define WGRT_TAIL_PREFETCH 0
-#endif
-constexpr int kPfSlots = 7;            // line 0 (80 B) in five 16-B slots, then the moves of branch a, b
-constexpr int kPfSlotWords = 64 * 4;   // one slot of a wave: 64 lanes x 16 B
-typedef unsigned U32x4 __attribute__((ext_vector_type(4)));
-
-__device__ __forceinline__ void glds16(const void *g, LdsU32 *dst) {
-    __builtin_amdgcn_global_load_lds(g, (void __attribute__((address_space(3))) *)dst, 16, 0, 0);
-}
-
-#define KAO(T, off) K.template get<T>(off)
-
-// The block a lane at (x, y) in region nreg will interact with next, if its next loop iteration is an
-// interaction: 1 + nreg for the in-coupler states, else the region's first block plus the predicted slice;
-// -1 for nreg < 0 or a coupler without a band model.
-__device__ __forceinline__ int predict_block(const KArgs &K, int nreg, double x, double y, int nfc, int noc) {
-    const bool fc = nreg <= 3;
-    constexpr size_t of = offsetof(TraceArgs, bfc), oo = offsetof(TraceArgs, boc);
-    // both couplers' values read (scalar loads) and then selected per lane: a select of the two kernarg
-    // addresses would be a per-lane address, i.e. a vector load, waited for behind the cell word
-    const double uxf = KAO(double, of + offsetof(SliceBands, ux)), uxo = KAO(double, oo + offsetof(SliceBands, ux));
-    const double uyf = KAO(double, of + offsetof(SliceBands, uy)), uyo = KAO(double, oo + offsetof(SliceBands, uy));
-    const double ux = fc ? uxf : uxo, uy = fc ? uyf : uyo;
-    const int nf = KAO(int, of + offsetof(SliceBands, ncut)), no = KAO(int, oo + offsetof(SliceBands, ncut));
-    const int ncut = fc ? nf : no;
-    const float t = (float)(x * ux + y * uy);
-    int sl = 0;
-    const int kmax = nf > no ? nf : no;
-    for (int k = 0; k < kmax; ++k) {
-        const float cf = KAO(float, of + offsetof(SliceBands, cut) + 4 * (size_t)k);
-        const float co = KAO(float, oo + offsetof(SliceBands, cut) + 4 * (size_t)k);
-        sl += (k < ncut) & (t > (fc ? cf : co));
-    }
-    const int count = fc ? nfc : noc;
-    const int blk = 3 + (fc ? 0 : 2 * nfc) + (nreg - (fc ? 2 : 4)) * count + sl;
-    return nreg < 0 ? -1 : nreg <= 1 ? 1 + nreg : ncut < 0 ? -1 : blk;
-}
-
-// The prefetch of block pb's line 0 and region nreg's two branch moves into this lane's LDS slots.
-__device__ __forceinline__ void prefetch_line0(const KArgs &K, uint32_t tix, int jtile_d, int pb, int nreg,
-                                               LdsU32 *pfb) {
-    if (pb < 0 || WGRT_TAIL_PREFETCH >= 2) return;
-    const double *T = KA(jtiles) + (size_t)tix * (size_t)jtile_d;
-    const double *B = T + kJHeader + kJBlock * pb;
-#pragma unroll
-    for (int k = 0; k < 5; ++k) glds16(B + 2 * k, pfb + k * kPfSlotWords);
-    const int kd = nreg <= 1 ? 0 : nreg - 1;
-    glds16(T + kJGap + (kd >= 3 ? 2 : 0), pfb + 5 * kPfSlotWords);
-    glds16(T + kJGap + (kd == 0 ? 4 : (kd >= 3 ? 6 : 2)), pfb + 6 * kPfSlotWords);
-}
-
-// Whether a taken in-coupler branch's new position is predicted inside the in-coupler (its disc).
-__device__ __forceinline__ bool predict_in_ic(const KArgs &K, double x, double y) {
-    constexpr size_t od = offsetof(TraceArgs, icd);
-    const double ex = x - KAO(double, od + offsetof(DiscHint, cx)), ey = y - KAO(double, od + offsetof(DiscHint, cy));
-    return ex * ex + ey * ey <= KAO(double, od + offsetof(DiscHint, r2));
-}
-
-// estimate32 from Hermitian forms already in registers (the prefetching interaction)
-__device__ __forceinline__ void estimate32h(JDecision &d, const float4 &h0, const float4 &h1, const float4 &h2,
-                                            const JRay &r, bool three, double inv, double f01, double inv_n_g,
-                                            const double4 &cw) {
-    const float er = (float)r.er, ei = (float)r.ei, mr = (float)r.mr, mi = (float)r.mi;
-    const float a = fmaf(er, er, ei * ei), b = fmaf(mr, mr, mi * mi);
-    const float cr = fmaf(er, mr, ei * mi), ci = fmaf(er, mi, -ei * mr);
-    const double q0 = (double)herm_form(h0, a, b, cr, ci), q1 = (double)herm_form(h1, a, b, cr, ci);
-    double q2 = 0.0;
-    if (three) q2 = (double)herm_form(h2, a, b, cr, ci);
-    d.a0 = q0 * cw.x * inv * f01;
-    d.a1 = q1 * cw.y * inv * f01;
-    d.a2 = three ? q2 * cw.z * inv * inv_n_g : 0.0;
-}
-
 // Amplification of the lanes' state discrepancy ("The bound, stated").  Both lanes apply
 // the same Jones matrix M to states that differ, up to a global phase, by a chordal distance eps; after the
 // normalisation the distance is at most a eps / (1 - eps / rho) (first order exact: a = |det M| |E|^2 /
@@ -1097,9 +1009,9 @@ __device__ __forceinline__ float amp_step(float amp, float pa, float nmin, doubl
 // abandoned.  The taken branch's field is always computed in double precision from its
 // double-precision matrix (loaded after the decision), so the carried Jones vector and ener
 // are the same values the all-double evaluation gives.
-template <bool SINGLE, bool AMP, bool PF = false, class Loc>
+template <bool SINGLE, bool AMP, class Loc>
 __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int blk,
-                                        int kind, bool entry, SegAcc *sg = nullptr, LdsU32 *pfb = nullptr) {
+                                        int kind, bool entry, SegAcc *sg = nullptr) {
     JRay &r = L.r;
     const double *T = KA(jtiles) + (size_t)L.tix * (size_t)A.jtile_d;
     const double *B = T + kJHeader + kJBlock * blk;
@@ -1112,44 +1024,11 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const int gb = kind == 0 ? 4 : (kind >= 3 ? 6 : 2);
     double growth, cos_ic1;
     bool amp_blk;
-    double4 cw;
-    double2 mva, mvb;
-    float4 hp[3];   // PF: the block's Hermitian forms
-    if (PF) {
-        U32x4 v[kPfSlots];
-        if (blk == L.pb) {   // prefetched: this lane's LDS slots (landed: the tail pass starts with vmcnt(0))
-            const U32x4 __attribute__((address_space(3))) *q =
-                (const U32x4 __attribute__((address_space(3))) *)pfb + (threadIdx.x & 63);
-#pragma unroll
-            for (int k = 0; k < kPfSlots; ++k) v[k] = q[64 * k];
-        } else {   // mispredicted (or none): the line-0 loads, waited for inside this branch
-#pragma unroll
-            for (int k = 0; k < 5; ++k) v[k] = *(const U32x4 *)(B + 2 * k);
-            v[5] = *(const U32x4 *)(T + kJGap + ga);
-            v[6] = *(const U32x4 *)(T + kJGap + gb);
-            // used here, so their vmcnt wait is placed inside this branch: a wait after the join would run
-            // on every pass and, vmcnt counting in issue order, wait for the miss hops' cell words too
-#pragma unroll
-            for (int k = 0; k < kPfSlots; ++k) asm volatile("" ::"v"(v[k]));
-        }
-        const double2 c01 = __builtin_bit_cast(double2, v[0]);
-        const float4 fw = __builtin_bit_cast(float4, v[1]);
-        hp[0] = __builtin_bit_cast(float4, v[2]);
-        hp[1] = __builtin_bit_cast(float4, v[3]);
-        hp[2] = __builtin_bit_cast(float4, v[4]);
-        mva = __builtin_bit_cast(double2, v[5]);
-        mvb = __builtin_bit_cast(double2, v[6]);
-        growth = (double)(entry ? fw.y : fw.z);
-        cos_ic1 = __hiloint2double(__float_as_int(fw.w), __float_as_int(fw.z));
-        amp_blk = __float_as_uint(fw.x) >> 31;
-        cw = double4{c01.x, c01.y, (double)fw.y, (double)fabsf(fw.x)};
-    } else {
-        cw = block_cw(B, entry, growth, cos_ic1, amp_blk);
-        // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
-        // issued together with its matrix, one memory round trip per interaction less
-        mva = *(const double2 *)(T + kJGap + ga);
-        mvb = *(const double2 *)(T + kJGap + gb);
-    }
+    const double4 cw = block_cw(B, entry, growth, cos_ic1, amp_blk);
+    // both branches' moves with the estimate's loads: the taken branch's new cell word can then be
+    // issued together with its matrix, one memory round trip per interaction less
+    const double2 mva = *(const double2 *)(T + kJGap + ga);
+    const double2 mvb = *(const double2 *)(T + kJGap + gb);
     const double denom = entry ? cos_ic1 : r.cos_t;
     const double u = rng_draw_lazy(r.s, [&]() { return ray_gid_ka(K, (int64_t)L.i); });
     const double inv = rcp_nr(denom);
@@ -1159,8 +1038,7 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     const double grow = AMP ? fma(nb * nb, growth, 1.0) * (double)r.amp : fma(nb * nb, growth, 1.0);
     const double base = grow * fabs(inv) * fmax(e2, 1.0);
     JDecision d;
-    if (PF) estimate32h(d, hp[0], hp[1], hp[2], r, three, inv, f01, A.inv_n_g, cw);
-    else estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg);
+    estimate32(d, B, r, three, inv, f01, A.inv_n_g, cw, sg);
     jones_decide(d, u, A.cert_tol32 * base, B, cw.w, three, thr, t, r.ener, SINGLE ? r.eerr : 0.0);
     if (__builtin_expect(!d.ok, 0)) {   // rare: the double-precision evaluation
         estimate64(d, B, r, three, inv, f01, A.inv_n_g, cw);
@@ -1181,13 +1059,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
     r.x = r.x + mv.x;
     r.y = r.y + mv.y;
     L.pf = locate_c(loc, r.x, r.y);
-    if (PF) {   // the next interaction's line 0, predicted from the new position and region
-        const int nreg = kind == 0 ? (predict_in_ic(K, r.x, r.y) ? (ba ? 0 : 1) : (ba ? 2 : -1))
-                                   : (kind <= 2 ? (ba ? 2 : 3) : (ba ? 4 : 5));
-        const int pb = predict_block(K, nreg, r.x, r.y, A.nfc, A.noc);
-        prefetch_line0(K, L.tix, A.jtile_d, pb, nreg, pfb);
-        L.pb = WGRT_TAIL_PREFETCH >= 2 ? pb + (1 << 30) : pb;
-    }
     // the phase step of the new region's miss hops (R2: 2 lut_TIR[0]; R3, R4: 2 lut_TIR[1]; the
     // in-coupler states and R5 never hop), loaded with the taken branch's matrix
     const double2 hop = *(const double2 *)(T + kJHop + ((kind == 0 || (kind <= 2 && ba)) ? 0 : 2));
@@ -1273,9 +1144,8 @@ __device__ __forceinline__ int low_bit(uint64_t v) { return __builtin_ctzll(v); 
 // evaluation per lane -- and only lanes whose outcome hinges on an EDGE class take the (rare)
 // exact path first: the earlier nested per-slice tests cost every wave-pass the exec-mask
 // bookkeeping of every slice's exact test (SALU per bounce).
-template <bool PF = false, class Loc>
-__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind,
-                                       LdsU32 *pfb = nullptr) {
+template <class Loc>
+__device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const Loc &loc, JLane &L, int &kind) {
     using W = typename Loc::Word;
     constexpr int kBits = 8 * (int)sizeof(W);
     constexpr W kLow = (W)0x5555555555555555ull;
@@ -1325,11 +1195,6 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
         r.mr = fma(mr, r.hr, -r.mi * r.hi);
         r.mi = fma(mr, r.hi, r.mi * r.hr);
         L.pf = locate_c(loc, r.x, r.y);   // read by the next pass
-    }
-    if (PF && (hop | sw)) {   // the launch tail: the next interaction's line 0 at the new position / region
-        const int pb = predict_block(K, sw ? 4 : region, r.x, r.y, nfc, noc);
-        prefetch_line0(K, L.tix, A.jtile_d, pb, sw ? 4 : region, pfb);
-        L.pb = WGRT_TAIL_PREFETCH >= 2 ? pb + (1 << 30) : pb;
     }
     const int step = hit ? blkbase + sl : kTransit;
     const int next = ic ? 1 + region : step;

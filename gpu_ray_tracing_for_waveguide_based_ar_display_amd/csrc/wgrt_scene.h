@@ -29,8 +29,6 @@ struct wgrt_scene {
     int64_t edge_cells = 0;        // locator cells with an EDGE class
     int jones_grid[2][2][2] = {};   // resident 256-thread workgroups: [64-bit cells][fused][single wavelength]
     int jones_tl_grid[2] = {};      // ... of the debug timeline instantiations (32-bit cells): [fused]
-    wgrt::SliceBands bfc, boc;      // the launch tail's line-0 prefetch hints (wgrt_scene_build.h)
-    wgrt::DiscHint icd;
     int64_t nonunitary_blocks = 0;  // Jones blocks whose branch matrices are not scaled-unitary (their launches
                                     // run the AMP instantiations: wgrt_device.h, the amplification step)
     // Jones-vector launches: per-stream launch scratch (launches on one stream are ordered, so

@@ -338,74 +338,4 @@ void build_scene_host(const wgrt_scene_desc &d, double cell_mm, SceneHost &out, 
     out.jtile_doubles = jtile_doubles((int)d.n_fc_slices, (int)d.n_oc_slices);
 }
 
-// ---------------------------------------------------------------------------------------------------
-// Slice bands (prediction hints for the launch tail's line-0 prefetch; wgrt_scene_build.h)
-// ---------------------------------------------------------------------------------------------------
-bool fit_slice_bands(const double *V, const int64_t *off, int n, SliceBands &out) {
-    out = SliceBands{};
-    if (n <= 0 || n - 1 > kMaxSliceCuts) return false;
-    if (n == 1) {   // one slice: nothing to cut
-        out.ncut = 0;
-        return true;
-    }
-    std::vector<double> px(n - 1), py(n - 1);   // a point on each cut
-    double dx0 = 0.0, dy0 = 0.0;
-    for (int k = 0; k + 1 < n; ++k) {
-        // the vertices slices k and k + 1 share (the band cuts are the same computed points on both sides)
-        std::vector<std::pair<double, double>> sh;
-        for (int64_t i = off[k]; i < off[k + 1]; ++i)
-            for (int64_t j = off[k + 1]; j < off[k + 2]; ++j)
-                if (std::fabs(V[2 * i] - V[2 * j]) <= 1e-9 && std::fabs(V[2 * i + 1] - V[2 * j + 1]) <= 1e-9)
-                    sh.push_back({V[2 * i], V[2 * i + 1]});
-        double best = 0.0, dx = 0.0, dy = 0.0;
-        for (size_t a = 0; a < sh.size(); ++a)
-            for (size_t b = a + 1; b < sh.size(); ++b) {
-                const double ex = sh[b].first - sh[a].first, ey = sh[b].second - sh[a].second;
-                if (ex * ex + ey * ey > best) best = ex * ex + ey * ey, dx = ex, dy = ey;
-            }
-        if (best < 1e-12) return false;   // no cut edge
-        const double l = std::sqrt(best);
-        dx /= l, dy /= l;
-        if (k == 0) {
-            dx0 = dx, dy0 = dy;
-        } else if (std::fabs(dx * dy0 - dy * dx0) > 1e-6) {
-            return false;   // not parallel
-        }
-        px[k] = sh[0].first, py[k] = sh[0].second;
-    }
-    double ux = -dy0, uy = dx0;
-    auto centre = [&](int k) {
-        double t = 0.0;
-        const int64_t m = off[k + 1] - off[k];
-        for (int64_t i = off[k]; i < off[k + 1]; ++i) t += ux * V[2 * i] + uy * V[2 * i + 1];
-        return m > 0 ? t / (double)m : 0.0;
-    };
-    if (centre(0) > centre(1)) ux = -ux, uy = -uy;
-    double prev = centre(0);
-    for (int k = 0; k + 1 < n; ++k) {
-        const double c = ux * px[k] + uy * py[k], nxt = centre(k + 1);
-        if (!(prev < c && c < nxt)) return false;   // the slices are not ordered bands
-        out.cut[k] = (float)c;
-        prev = nxt;
-    }
-    out.ux = ux, out.uy = uy;
-    out.ncut = n - 1;
-    return true;
-}
-
-DiscHint fit_disc(const double *V, int64_t nv) {
-    DiscHint d;
-    if (nv < 3) return d;
-    double cx = 0.0, cy = 0.0;
-    for (int64_t i = 0; i < nv; ++i) cx += V[2 * i], cy += V[2 * i + 1];
-    cx /= (double)nv, cy /= (double)nv;
-    double r2 = 1e300;
-    for (int64_t i = 0; i < nv; ++i) {
-        const double ex = V[2 * i] - cx, ey = V[2 * i + 1] - cy;
-        r2 = std::min(r2, ex * ex + ey * ey);
-    }
-    d.cx = cx, d.cy = cy, d.r2 = r2;
-    return d;
-}
-
 }  // namespace wgrt

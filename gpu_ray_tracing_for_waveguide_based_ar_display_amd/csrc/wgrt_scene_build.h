@@ -30,25 +30,6 @@ struct LocatorHost {
     int64_t edge_cells = 0;
 };
 
-// A coupler's slices as parallel bands, for PREDICTING which slice a position falls in (the launch
-// tail's line-0 prefetch, wgrt_trace.hip): the cut lines between consecutive slices share a direction,
-// so a slice is a range of the projection t = u . (x, y) on their normal.  Only a hint: the kernel
-// confirms every prediction against the cell word and loads the right block when it missed.
-constexpr int kMaxSliceCuts = 31;
-struct SliceBands {
-    double ux = 1.0, uy = 0.0;     // unit normal of the cuts, oriented so t increases with the slice index
-    float cut[kMaxSliceCuts] = {}; // t of the cut between slice k and k + 1
-    int ncut = -1;                 // slices - 1; -1: no band model (the slices are not parallel bands)
-};
-// The in-coupler as a disc (a hint again: whether a taken in-coupler branch stays in it).
-struct DiscHint {
-    double cx = 0.0, cy = 0.0, r2 = -1.0;   // r2 < 0: none
-};
-// Fit the bands of polygons verts[off[k] .. off[k+1]) (k < n, [V][2] doubles); false (out.ncut = -1) if the
-// consecutive slices do not share parallel cut edges.
-bool fit_slice_bands(const double *verts, const int64_t *off, int n, SliceBands &out);
-DiscHint fit_disc(const double *verts, int64_t nv);
-
 struct SceneHost {
     LocatorHost loc;
     std::vector<double> tiles;     // [num_lmd * nx * ny][tile_doubles]

@@ -216,13 +216,6 @@ constexpr int64_t kStripe = WGRT_STRIPE;
 #define SEG_TMARK(sg, k, dep) ((void)0)
 #endif
 
-// The launch tail's line-0 prefetch (wgrt_device.h prefetch_line0).
-constexpr bool kTailPrefetch = WGRT_TAIL_PREFETCH != 0;
-template <bool B>
-struct BoolC {
-    static constexpr bool value = B;
-};
-
 #ifndef WGRT_ONE_RETIRE
 #define WGRT_ONE_RETIRE 1
 #endif
@@ -398,10 +391,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     };
     // this wave's two LDS buffers of staged ray columns (wgrt_device.h stage_chunk): a refill takes
     // rays of at most two chunks, the one being used up and the next
-    // (in the launch tail the same LDS holds the wave's line-0 prefetch slots: kPfSlots x 64 lanes x 16 B)
-    constexpr int kStageWave = 2 * kStageCols * 64 > kPfSlots * kPfSlotWords ? 2 * kStageCols * 64 : kPfSlots * kPfSlotWords;
-    __shared__ uint32_t stage_buf[4][kStageWave];
-    LdsU32 *const sbufs = (LdsU32 *)&stage_buf[threadIdx.x >> 6][0];
+    __shared__ uint32_t stage_buf[4][2][kStageCols * 64];
+    LdsU32 *const sbufs = (LdsU32 *)&stage_buf[threadIdx.x >> 6][0][0];
     // wave-uniform: the buffer of the current item, its first ray and the previous item's first
     // ray (the other buffer).  A taken lane finds its slot from its ray index: items are disjoint
     // ranges of at most 64 rays.
@@ -548,9 +539,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
     };
 
     // the second half of a pass: the interaction of the lanes at one, and this pass's out-couplings
-    // pf: BoolC<true> in the launch tail (the line-0 prefetch, wgrt_device.h), BoolC<false> elsewhere
-    auto interact_pass = [&](SegAcc *sg, auto pf) {
-        constexpr bool PF = decltype(pf)::value;
+    auto interact_pass = [&](SegAcc *sg) {
         if (TL && tl_on) {
             ++tl_passes;
             tl_lanes += __popcll(__ballot(active));
@@ -558,7 +547,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         bool out = false;
         if (active && blk >= 0) {
             L.inter += entry ? 0u : 1u;
-            const int next = interact<SINGLE, AMP, PF>(A, K, loc, L, blk, kind, entry, sg, PF ? sbufs : nullptr);
+            const int next = interact<SINGLE, AMP>(A, K, loc, L, blk, kind, entry, sg);
             out = next == kOut;
             outcome(next);
         }
@@ -688,7 +677,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // single-trace launches: once the queue has run dry, the wave's remaining rays finish in
         // the tail loop below
         if (!FUSED && exhausted) break;
-        interact_pass(nullptr, BoolC<false>{});
+        interact_pass(nullptr);
     }
     if (!FUSED && __ballot(active) != 0ull) {
         // the launch tail: the same passes without the refill.  A loop of its own, so the rays in
@@ -696,6 +685,8 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // (-1.6 % per single launch on C3).  Issuing both branches' matrices or both candidate
         // cell words before the decision here (one or two round trips less per interaction) lost
         // 1.5 % and 6 %: the chip is still full of rays when the queue runs dry.
+        // Prefetching the next interaction's line 0 into LDS at each move, its block predicted from
+        // the new position (round 6, commit 6b094d1), lost 18-48 %.
         // The first pass continues the one the main loop broke off (advance and refill done).
 #ifdef WGRT_SEG
         __shared__ uint32_t seg_lds[4][16];
@@ -705,15 +696,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 #else
         SegAcc *const sg = nullptr;
 #endif
-        if (kTailPrefetch) {
-            L.pb = -1;   // nothing prefetched yet; the staging reads of the last refill are done
-            asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        }
         for (bool first = true;; first = false) {
-            // the prefetches of the last pass have landed before this pass reads its LDS slots (and before
-            // this pass's own prefetches overwrite them)
-            // (the builtin, not inline asm: the compiler's wait insertion then knows that nothing is in flight)
-            if (kTailPrefetch && WGRT_TAIL_PREFETCH != 3) __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) alone (gfx9 encoding)
 #ifdef WGRT_SEG
             if (sg) {
                 const uint32_t t0 = seg_stamp();
@@ -721,7 +704,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
             }
 #endif
             if (!first && active) {
-                blk = advance<kTailPrefetch>(A, K, loc, L, kind, kTailPrefetch ? sbufs : nullptr);
+                blk = advance(A, K, loc, L, kind);
                 entry = false;
                 if (ONE) fin |= blk == kDie;
                 else if (blk == kDie) retire();
@@ -736,7 +719,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 #ifdef WGRT_SEG
             if (seg_first_lane()) seg.p[7] += 1u;
 #endif
-            interact_pass(sg, BoolC<kTailPrefetch>{});
+            interact_pass(sg);
         }
 #ifdef WGRT_SEG
         // segment sums: words 8..15 of a 16-word wave record (tools/segments.py)
@@ -1175,10 +1158,6 @@ wgrt_status wgrt_scene_create_ex(const wgrt_scene_desc *desc, int device, const 
     s->nl = d.num_lmd;
     s->nfc = (int)d.n_fc_slices;
     s->noc = (int)d.n_oc_slices;
-    // the launch tail's prefetch hints (wgrt_scene_build.h): the slices as bands, the in-coupler as a disc
-    fit_slice_bands(d.FC, d.FC_offset, s->nfc, s->bfc);
-    fit_slice_bands(d.OC, d.OC_offset, s->noc, s->boc);
-    s->icd = fit_disc(d.IC, d.n_ic);
     s->tile_d = host.tile_doubles;
     s->jtile_d = host.jtile_doubles;
     s->npoly = 3 + s->nfc + s->noc;
@@ -1588,9 +1567,6 @@ wgrt_status trace_launch(const wgrt_scene *s, const wgrt_rays *rays, int64_t n_r
     A.timeline_waves = timeline ? dbg->timeline_waves : 0;
     A.jtiles = s->d_jtiles;
     A.jtile_d = s->jtile_d;
-    A.bfc = s->bfc;
-    A.boc = s->boc;
-    A.icd = s->icd;
     A.n_iter = 1;
     hipStream_t st = (hipStream_t)stream;
     if (variant == 1) {
