@@ -86,6 +86,13 @@ PROFILES = {
     "adversarial_rank1": dict(ic=(0.40, 0.05), r0=(0.85, 0.05), r1=(0.05, 0.85),
                               fc_fold=(0.08, 0.30), fc_keep=0.97, fc_back=0.04, fc2_keep=0.93,
                               oc_turn=0.03, oc_out=(0.06, 0.25), oc_keep=0.96, jones="singular", cond=1e9),
+    # * moderately polarisation-selective matrices (rank one plus 1/10 of a unitary one, condition ~10):
+    #   unlike the two above, a ray's state often lies nearer a taken matrix's weak direction than its
+    #   strong one, so the amplification factor a = |det M| |E|^2 / |M E|^2 exceeds 1 on a sizeable share
+    #   of interactions and the amplification-tracked bound grows along a ray;
+    "adversarial_polarizing": dict(ic=(0.40, 0.05), r0=(0.85, 0.05), r1=(0.05, 0.85),
+                                   fc_fold=(0.08, 0.30), fc_keep=0.97, fc_back=0.04, fc2_keep=0.93,
+                                   oc_turn=0.03, oc_out=(0.06, 0.25), oc_keep=0.96, jones="singular", cond=10.0),
     # * lossless interactions whose branch efficiencies sum to 1 - 1e-9 and split (nearly) evenly, no
     #   jitter: every interaction's last threshold sits 1e-9 below 1 (draws near 1 decide against it)
     #   and the branch thresholds sit near the common draw 0.5; with shortened hops (tests scale

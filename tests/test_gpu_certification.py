@@ -118,6 +118,10 @@ def test_shadow_follows_reference(dev):
                             gap_scale=0.05, tir_near_pi=True)),
     ("adv_rank1_single_guard", dict(nx=7, ny=7, lambdas=[2], R=4096, profile="adversarial_rank1",
                                     gap_scale=0.25, wavelength=2)),
+    # condition ~10: the amplification factor exceeds 1 often, so the tracked bound does grow
+    ("adv_polarizing_C3", dict(nx=21, ny=21, lambdas=[0, 1, 2], R=1024, profile="adversarial_polarizing")),
+    ("adv_polarizing_deep", dict(nx=11, ny=11, lambdas=[0, 1, 2], R=4096, profile="adversarial_polarizing",
+                                 gap_scale=0.05, tir_near_pi=True)),
 ])
 def test_certification_slack(dev, name, cfg):
     st, *_ = _shadow_run(dev, **cfg)
@@ -127,6 +131,8 @@ def test_certification_slack(dev, name, cfg):
     assert st["silent_flips"] == 0
     if not name.startswith("adv_"):
         assert st["max_amp"] <= 1.0, st   # scaled-unitary LUTs: the amplification step never runs
+    if name.startswith("adv_polarizing"):
+        assert st["max_amp"] > 1.0, st    # the amplification step ran, and the bound it scales held
     assert st["max_ratio"] <= 1e-2, st      # double-precision evaluation vs its bound
     assert st["max_ratio32"] <= 0.5, st     # single-precision estimate vs its bound
     # the double-precision re-evaluation is correct, only slower; the lossless long-phase profile's rays
@@ -155,6 +161,9 @@ def test_certification_slack(dev, name, cfg):
     ("adv_rank1", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_rank1")),
     ("adv_rank1_deep", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_rank1",
                             gap_scale=0.05, tir_near_pi=True)),
+    ("adv_polarizing", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_polarizing")),
+    ("adv_polarizing_deep", dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_polarizing",
+                                 gap_scale=0.05, tir_near_pi=True)),
 ])
 @pytest.mark.parametrize("variant", [7, 9, 1])
 def test_adversarial_luts_match_oracle(dev, name, cfg, variant):

@@ -80,7 +80,7 @@ def test_device_scene_equals_host_build(lib, nx, ny, profile, wl):
 
 
 @pytest.mark.parametrize("profile,flagged", [("default", False), ("stress", False), ("adversarial_singular", True),
-                                             ("adversarial_rank1", True)])
+                                             ("adversarial_rank1", True), ("adversarial_polarizing", True)])
 def test_nonunitary_blocks_flagged(lib, profile, flagged):
     """The sign bit of a Jones block's float Wsum (wgrt_pack.h) flags a block whose taken branches' matrices are
     not scaled-unitary (kappa^2 > 1 + 1e-6): the Jones lane runs its amplification step there only.  The
