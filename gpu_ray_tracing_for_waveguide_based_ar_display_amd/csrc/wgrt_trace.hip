@@ -803,6 +803,9 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         if (t_bad) atomicAdd(acc + 1, t_bad);
         if (t_h) atomicAdd(acc + 2, t_h);
         if (t_i) atomicAdd(acc + 3, t_i);
+        // gfx9: vmcnt counts the no-return atomics too, so they have been performed at the device-coherent
+        // level before the done count below; an acq_rel increment instead would write back this XCD's
+        // whole L2 (buffer_wbl2) per workgroup for values that never sit in it
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         last_wg = atomicAdd(KA(epi_done), 1ull) == (unsigned long long)gridDim.x - 1ull;
     }
