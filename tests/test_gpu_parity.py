@@ -101,6 +101,9 @@ def _config(nx, ny, lambdas, R, seed=0, profile="default", point_seed=1, wavelen
     dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="deep", seed=5),
     dict(nx=11, ny=11, lambdas=[1], R=1024, wavelength=1),           # single-wavelength kernel, C2 size
     dict(nx=7, ny=7, lambdas=[2], R=512, profile="balanced", gap_scale=0.25, wavelength=2),  # 1e-15 guard
+    # non-unitary Jones matrices: the amplification-tracked (AMP) instantiations, full colour and single-λ
+    dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="adversarial_polarizing", seed=3),
+    dict(nx=7, ny=7, lambdas=[2], R=512, profile="adversarial_polarizing", gap_scale=0.25, wavelength=2),
 ])
 @pytest.mark.parametrize("variant", VARIANTS)
 def test_matches_oracle_at_scale(dev, cfg, variant):
@@ -123,11 +126,15 @@ def test_matches_oracle_at_scale(dev, cfg, variant):
 @pytest.mark.parametrize("cfg", [dict(nx=11, ny=11, lambdas=[1], R=256),
                                  dict(nx=9, ny=7, lambdas=[0, 1, 2], R=256, profile="deep", seed=5),
                                  dict(nx=7, ny=7, lambdas=[2], R=512, profile="balanced", gap_scale=0.25,
-                                      wavelength=2)])
+                                      wavelength=2),
+                                 # AMP instantiation: a raised bound also trips the amplification step's
+                                 # near-singular-branch check (|M E|^2 below 1e6 q^2 tr(H) |E|^2)
+                                 dict(nx=9, ny=7, lambdas=[0, 1, 2], R=256, profile="adversarial_polarizing",
+                                      seed=3)])
 def test_replay_path_forced(dev, cfg, cert_tol):
     """The Jones-vector variants' rare branch (SURVEY-style rule: a rare data-dependent branch
     needs its own test): a large certification bound makes many decisions uncertain, so many
-    rays are abandoned and re-traced by replay_kernel -- results must still equal the oracle
+    rays are abandoned and re-traced by the replay (single launches: inside the trace kernel) -- results must still equal the oracle
     bit for bit, and the replay counter must show the branch ran."""
     from oracle import OracleScene
     c = _config(**cfg)
@@ -210,6 +217,7 @@ def test_fused_iterations_golden(dev, name, variant):
     dict(nx=21, ny=21, lambdas=[0, 1, 2], R=128),
     dict(nx=9, ny=7, lambdas=[0, 1, 2], R=512, profile="deep", seed=5),
     dict(nx=7, ny=7, lambdas=[2], R=512, profile="balanced", gap_scale=0.25, wavelength=2),
+    dict(nx=9, ny=7, lambdas=[0, 1, 2], R=256, profile="adversarial_polarizing", seed=3),   # fused AMP kernels
 ])
 @pytest.mark.parametrize("num_iter,variant,cert_tol", [(3, 7, None), (5, 9, None), (3, 7, 1e-4), (2, 9, 1e-2)])
 def test_fused_iterations_match_oracle(dev, cfg, num_iter, variant, cert_tol):
