@@ -1111,6 +1111,9 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
 // The EDGE classes a lane's loop iteration consults -- eff_reg1's, the region's slices' up to the
 // first IN one, eff_reg2's in R3 -- replaced by the exact predicate's verdict (IN 1 / OUT 0) through
 // the 128-B band records (in_poly_w).  Rare: 0.34 % of C3 lane-passes meet an EDGE cell.
+#ifndef WGRT_EDGE_WAIT
+#define WGRT_EDGE_WAIT 1
+#endif
 template <class Loc>
 __device__ __forceinline__ typename Loc::Word resolve_edges(const KArgs &K, const Loc &loc, typename Loc::Word w,
                                                             int region, int first, int count, double x, double y) {
@@ -1165,6 +1168,13 @@ __device__ __forceinline__ int advance(const TraceArgs &A, const KArgs &K, const
     const bool e2edge = region == 3 && cand == 0 && ((c >> (2 * kPolyEff2)) & 3u) == 2u;
     if (__builtin_expect(e1edge | sedge | e2edge, 0)) {
         c = resolve_edges(K, loc, c, region, first, count, r.x, r.y);
+        // the band records' loads have all landed (a compiler-visible vmcnt(0), gfx9 encoding): an exit of the
+        // exact test that leaves some in flight would otherwise make the wait insertion assume them pending
+        // on every path after this rare one, and wait for every load in flight before the interaction's
+        // line-0 loads -- the pass's miss-hop gathers among them
+#if WGRT_EDGE_WAIT
+        __builtin_amdgcn_s_waitcnt(0x0F70);
+#endif
         f = (c >> (2 * first)) & gmask;
         in = f & kLow;
         cand = in | ((f >> 1) & kLow);

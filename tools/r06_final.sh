@@ -15,7 +15,7 @@ stop $? smoke
 cp profiles/traffic.json "$OUT/traffic.json"; cp profiles/pmc.json "$OUT/pmc.json"
 timeout -k 10 600 python tools/pmc_traffic.py "$OUT/traffic.json" > "$OUT/traffic.log" 2>&1
 stop $? traffic
-TAG=r06f/run timeout -k 10 900 bash tools/pmc_passes.sh > "$OUT/pmc.log" 2>&1
+TAG=${FINAL_TAG:-r06f}/run timeout -k 10 900 bash tools/pmc_passes.sh > "$OUT/pmc.log" 2>&1
 stop $? pmc
 python tools/pmc_summary.py "$OUT/run_pmc" "$OUT/pmc_summary.json" --merge "$OUT/pmc.json" >> "$OUT/pmc.log" 2>&1
 stop $? pmc_summary
