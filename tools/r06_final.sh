@@ -4,7 +4,7 @@
 # a rocprofv3 kernel-trace summary, the other configs' lines and the 2-rank rehearsal.
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
 ROOT=$(pwd)
-OUT=$ROOT/gpurun_out/r06f
+OUT=$ROOT/gpurun_out/${FINAL_TAG:-r06f}
 mkdir -p "$OUT"
 export TMPDIR=/tmp
 stop() { echo "[$2] exit $1"; [ "$1" -ne 0 ] && exit "$1"; return 0; }
