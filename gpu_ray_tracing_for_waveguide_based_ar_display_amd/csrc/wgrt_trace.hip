@@ -570,7 +570,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 
     for (;;) {
 #if WGRT_MAIN_TOPWAIT
-        __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) alone (gfx9 encoding)
+        __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
         if (active) {
             blk = advance(A, K, loc, L, kind);
@@ -679,7 +679,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
         // their columns however many items they came from
         if (staged) {
 #if WGRT_MAIN_TOPWAIT
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // the staging loads have landed (vmcnt(0); the builtin, so
+            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);   // the staging loads have landed (the builtin, so
             asm volatile("" ::: "memory");        // the compiler's wait insertion knows nothing is in flight)
 #else
             asm volatile("s_waitcnt vmcnt(0)" ::: "memory");   // the staging loads have landed
@@ -718,7 +718,7 @@ __device__ __forceinline__ void jones_body(const TraceArgs &A, const KArgs &K, c
 #endif
         for (bool first = true;; first = false) {
 #if WGRT_TAIL_TOPWAIT
-            __builtin_amdgcn_s_waitcnt(0x0F70);   // vmcnt(0) alone (gfx9 encoding)
+            __builtin_amdgcn_s_waitcnt(kWaitVmcnt0);
 #endif
 #ifdef WGRT_SEG
             if (sg) {
