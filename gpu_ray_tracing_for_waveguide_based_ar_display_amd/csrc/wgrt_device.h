@@ -15,6 +15,11 @@
 
 namespace wgrt {
 
+// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima, in the gfx9 simm16 encoding (vmcnt bits
+// 3:0 and 15:14, expcnt 6:4 = 7, lgkmcnt 11:8 = 15): through __builtin_amdgcn_s_waitcnt, so the compiler's
+// wait insertion knows that every vector-memory access issued before it has completed
+constexpr int kWaitVmcnt0 = 0x0F70;
+
 // ----------------------------------------------------------------------------
 // device-side scene view
 // ----------------------------------------------------------------------------
@@ -1114,10 +1119,6 @@ __device__ __forceinline__ int interact(const TraceArgs &A, const KArgs &K, cons
 #ifndef WGRT_EDGE_WAIT
 #define WGRT_EDGE_WAIT 1
 #endif
-// s_waitcnt vmcnt(0) with expcnt / lgkmcnt left at their maxima, in the gfx9 simm16 encoding (vmcnt bits
-// 3:0 and 15:14, expcnt 6:4 = 7, lgkmcnt 11:8 = 15): through __builtin_amdgcn_s_waitcnt, so the compiler's
-// wait insertion knows that every vector-memory access issued before it has completed
-constexpr int kWaitVmcnt0 = 0x0F70;
 template <class Loc>
 __device__ __forceinline__ typename Loc::Word resolve_edges(const KArgs &K, const Loc &loc, typename Loc::Word w,
                                                             int region, int first, int count, double x, double y) {
